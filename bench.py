@@ -1,0 +1,269 @@
+#!/usr/bin/env python3
+"""bench.py -- qsfs MD5 chunk-hashing path on MI355X (BASELINE.json metric).
+
+Workload (BASELINE config 2): per GPU, a batch of 512 chunks
+of 10 MiB (10 485 760 B), device-resident in HBM, chunk i = LCG(12345 + i)
+(generated on the device before timing).  One step = one pass
+of the hot path over the batch: qsmd5_hash_batch_device_async (the gfx950
+kernel) producing all 512 digests, plus, for N > 1 GPUs, the RCCL all-gather
+of the 16-byte digests (rank r holds parts [512 r, 512 (r+1)) of the job).
+
+  python bench.py --gpus N --steps K --warmup W
+
+prints ONE JSON line (rank 0) with value = whole-job GiB/s hashed, the
+roofline of the dominant kernel (HIP events on the launch stream) and the CPU
+baseline (the reference's own md5() built from /root/reference into
+oracle/_ref, or the oracle port if that build is absent) timed on this host's
+cores over the same 512 chunks -- which also re-checks every GPU digest
+against the reference on the box.  Digests are checked against the committed
+golden fixture (tests/golden/batch_10MiB.json) every run.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "qsfs-fuse_amd"))
+
+MiB = 1 << 20
+CHUNK = 10 * MiB
+BATCH = 512
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+METRIC = "GiB/s MD5-hashed, device-resident 10 MB chunks, batch=512; % HBM-read peak"
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(host_chunks, gpu_hex, threads):
+    """Time the reference md5() (or the oracle port) on this host over the chunks."""
+    n = len(host_chunks)
+    ptrs = (ctypes.c_void_p * n)(*host_chunks)
+    lens = (ctypes.c_uint64 * n)(*([CHUNK] * n))
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_md5.so")
+    if os.path.exists(ref_so):
+        R = ctypes.CDLL(ref_so)
+        R.ref_md5_prepare.restype = ctypes.c_void_p
+        R.ref_md5_prepare.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        R.ref_md5_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        R.ref_md5_release.argtypes = [ctypes.c_void_p]
+        h = R.ref_md5_prepare(ptrs, lens, n)
+        out = (ctypes.c_char * (33 * n))()
+        t0 = time.perf_counter()
+        R.ref_md5_run(h, out, threads, 0)
+        dt = time.perf_counter() - t0
+        # single-thread sample of 16 chunks for the as-deployed (serial per file) rate
+        h1 = R.ref_md5_prepare(ptrs, lens, 16)
+        out1 = (ctypes.c_char * (33 * 16))()
+        t1 = time.perf_counter()
+        R.ref_md5_run(h1, out1, 1, 0)
+        dt1 = time.perf_counter() - t1
+        R.ref_md5_release(h1)
+        R.ref_md5_release(h)
+        raw = bytes(out)
+        ref_hex = [raw[33 * i:33 * i + 32].decode() for i in range(n)]
+        kind, what = "reference", "reference md5(std::string) (src/base/MD5.cpp:335-339, -O2)"
+    else:
+        O = ctypes.CDLL(os.path.join(ROOT, "oracle", "libmd5_oracle.so"))
+        O.oracle_md5_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                       ctypes.c_void_p, ctypes.c_int]
+        out = (ctypes.c_uint8 * (16 * n))()
+        t0 = time.perf_counter()
+        O.oracle_md5_batch(ptrs, lens, n, out, threads)
+        dt = time.perf_counter() - t0
+        out1 = (ctypes.c_uint8 * (16 * 16))()
+        t1 = time.perf_counter()
+        O.oracle_md5_batch(ptrs, lens, 16, out1, 1)
+        dt1 = time.perf_counter() - t1
+        raw = bytes(out)
+        ref_hex = [raw[16 * i:16 * i + 16].hex() for i in range(n)]
+        kind, what = "port", "oracle/md5_oracle.c (-O3)"
+    gib = n * CHUNK / float(1 << 30)
+    agree = ref_hex == gpu_hex
+    return {
+        "value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+        "sample": "%s over the same %d x 10 MiB chunks on %d threads (%.1f core-s); "
+                  "1 thread (as deployed: parts hashed serially) %.3f GiB/s on 16 chunks; "
+                  "host %s, %d CPUs visible" % (
+                      what, n, threads, dt * threads, 16 * CHUNK / float(1 << 30) / dt1,
+                      _cpu_model(), os.cpu_count() or 0),
+        "agrees_with_gpu": agree,
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _traffic_from_profiles():
+    """HBM bytes per launch from the committed PMC summary (profiles/*traffic*.json)."""
+    pdir = os.path.join(ROOT, "profiles")
+    best = None
+    if os.path.isdir(pdir):
+        for f in sorted(os.listdir(pdir)):
+            if f.endswith("_traffic.json"):
+                best = os.path.join(pdir, f)
+    if not best:
+        return None
+    try:
+        d = json.load(open(best))
+        if d.get("workload") == "batch512x10MiB":
+            return d.get("hbm_read_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=BATCH, help="chunks per GPU (default 512)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import qsmd5
+    from qsmd5.parallel import gather_digests
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (the MD5 path has no CPU fallback)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    rc = qsmd5.lib().qsmd5_init(0)
+    if rc != 0:
+        raise SystemExit("qsmd5_init failed: %d" % rc)
+
+    B, L = args.batch, CHUNK
+    stream = torch.cuda.current_stream()
+    sp = stream.cuda_stream
+    # --- synthetic device-resident input: chunk j of the job = LCG(12345 + j) --------
+    data = torch.empty(B * L, dtype=torch.uint8, device=dev)
+    seed0 = 12345 + rank * B
+    qsmd5.synth_fill_lcg(data.data_ptr(), L, L, seed0, B, sp)
+    desc = torch.empty((B, 2), dtype=torch.int64)
+    desc[:, 0] = data.data_ptr() + torch.arange(B, dtype=torch.int64) * L
+    desc[:, 1] = L
+    desc = desc.to(dev)
+    dig = torch.zeros((B, 16), dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    kernel = "producer/consumer (qsmd5_batch_pc_kernel)" if qsmd5.kernel_choice(B) == 1 else \
+        "one-wave (qsmd5_batch_kernel)"
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        qsmd5.hash_device(desc.data_ptr(), dig.data_ptr(), B, stream=sp)
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            return gather_digests(dig, B * world)
+        return dig
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for k in range(args.steps):
+        out = step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kernel_ms = [a.elapsed_time(b) for a, b in events]
+    kavg_ms = sum(kernel_ms) / len(kernel_ms)
+
+    # --- parity: every digest of the job against the reference-produced fixture -------
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_10MiB.json")))["md5"]
+    table = out if out is not None else dig
+    got_hex = [bytes(r).hex() for r in table.cpu().numpy()]
+    ntot = B * world
+    parity_ok = ntot <= len(gold) and got_hex[:ntot] == gold[:ntot]
+    if rank == 0 and not parity_ok:
+        bad = [i for i in range(min(ntot, len(gold))) if got_hex[i] != gold[i]]
+        log("PARITY FAILURE: %d of %d digests differ (first %s)" % (len(bad), ntot, bad[:5]))
+
+    job_bytes = float(ntot) * L
+    value = job_bytes / (1 << 30) / elapsed * args.steps
+    ms_per_step = elapsed / args.steps * 1e3
+    achieved_gbs = B * L / (kavg_ms * 1e-3) / 1e9
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: LCG(12345+i) chunks generated on device, resident in HBM",
+        "config": {"workload": "batch=%d x 10 MiB chunks per GPU, device-resident "
+                               "(BASELINE config 2)" % B,
+                   "global_batch": ntot, "chunk_bytes": L,
+                   "parallelism": "part-shard x%d + RCCL digest all-gather" % world
+                   if world > 1 else "single GPU", "kernel": kernel},
+        "roofline": {"bound": "hbm", "achieved": round(achieved_gbs, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved_gbs / HBM_PEAK_GBS, 5),
+                     "traffic": _traffic_from_profiles(),
+                     "kernel_ms_avg": round(kavg_ms, 3),
+                     "algorithmic_bytes_per_launch": B * L},
+        "per_chain": {"GiBps": round(B * L / (1 << 30) / (kavg_ms * 1e-3) / B, 4),
+                      "cycles_per_64B_block_at_2p4GHz": round(kavg_ms * 1e-3 * 2.4e9 / (L / 64), 1),
+                      "note": "MD5 is a serial chain per chunk; at batch=512 the job rate is "
+                              "512 x the per-chain rate (SURVEY.md §0 item 5)"},
+        "parity": "ok: %d/%d digests == reference golden" % (ntot, ntot) if parity_ok else "FAIL",
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        host = data.cpu().numpy()
+        chunks = [host[i * L:(i + 1) * L].ctypes.data for i in range(B)]
+        cb = cpu_baseline(chunks, got_hex[:B], threads)
+        result["cpu_baseline"] = cb
+        if not cb["agrees_with_gpu"]:
+            result["parity"] = "FAIL (cpu reference disagrees)"
+        del host
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0 if parity_ok else 3
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,167 @@
+/*
+ * include/qsmd5.h -- C-ABI of the MI355X MD5 chunk-hashing path for qsfs.
+ *
+ * Drop-in boundary for the reference's per-part Content-MD5 computation
+ * (qingstor-incubating/qsfs-fuse v1.0.11):
+ *
+ *   std::string md5(const boost::shared_ptr<std::iostream>&)  src/base/MD5.h:96,
+ *                                                              src/base/MD5.cpp:341-349
+ *   std::string md5(const std::string)                         src/base/MD5.h:95,
+ *                                                              src/base/MD5.cpp:335-339
+ *   class MD5 { update(); finalize(); hexdigest(); }           src/base/MD5.h:51-93
+ *
+ * called from QSClient::UploadMultipart (src/client/QSClient.cpp:369-371) and
+ * QSClient::UploadFile (src/client/QSClient.cpp:445-447).  The batch entry
+ * points add what the reference lacks: one call that hashes every part of a
+ * file (QSTransferManager::PrepareUpload / DoMultiPartUpload,
+ * src/client/QSTransferManager.cpp:475-550, 602-673).
+ *
+ * Contract (all entry points):
+ *   - extern "C", never throw, thread-safe, reentrant from any thread;
+ *   - return 0 on success or a negative errno (-EINVAL, -ENODEV, -ENOMEM,
+ *     -EIO); qsmd5_strerror() / qsmd5_last_error() describe failures;
+ *   - digests are the 16 raw MD5 bytes (RFC 1321 byte order), identical to
+ *     the reference's MD5::digest; qsmd5_hex() gives its hexdigest() text;
+ *   - hashing runs on the GPU only.  There is no CPU fallback: with no usable
+ *     device every hashing call fails with -ENODEV.  (The reference had no
+ *     error path; callers map a failure to QSError and retry the part.)
+ *   - lengths up to 2^38 bytes per chunk; the full 64-bit MD5 length is used.
+ *     The reference truncates lengths >= 4 GiB (MD5.h:53 32-bit size_type,
+ *     MD5.cpp:106); set QSMD5_FLAG_REF_TRUNCATE32 to reproduce that.
+ *
+ * Lazily initialised: the first call (or qsmd5_init) picks the current HIP
+ * device, so it is safe to call after fuse_main() has forked (reference
+ * Operations.cpp:1520-1549 initialises threads after the fork for the same
+ * reason).
+ */
+#ifndef QSMD5_H_
+#define QSMD5_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__)
+#define QSMD5_API __attribute__((visibility("default")))
+#else
+#define QSMD5_API
+#endif
+
+#define QSMD5_ABI_VERSION 1
+
+/* One message to hash: `len` bytes at `ptr`.  `ptr` may point to device
+ * memory (hipMalloc), pinned host memory (qsmd5_alloc_pinned / hipHostMalloc)
+ * or ordinary pageable host memory, at any byte alignment; NULL only if
+ * len == 0.  Layout-compatible with the kernel's descriptor. */
+typedef struct qsmd5_chunk {
+  const void* ptr;
+  uint64_t len;
+} qsmd5_chunk;
+
+/* One multipart-upload part, as QSTransferManager::PrepareUpload slices a
+ * file (QSTransferManager.cpp:475-550; Part, TransferHandle.h:45-101). */
+typedef struct qsmd5_part {
+  uint32_t part_number; /* 1-based, as the reference's part id */
+  uint32_t reserved;
+  uint64_t offset;      /* byte offset of the part in the file */
+  uint64_t size;        /* bytes in the part */
+} qsmd5_part;
+
+/* Flags for qsmd5_init / qsmd5_hash_batch_ex. */
+#define QSMD5_FLAG_NONE 0
+#define QSMD5_FLAG_REF_TRUNCATE32 1 /* hash only len mod 2^32 bytes, like MD5(std::string) */
+
+/* Initialise the runtime on the current HIP device (idempotent).  Returns 0,
+ * or -ENODEV when no GPU is usable. */
+QSMD5_API int qsmd5_init(int flags);
+
+QSMD5_API int qsmd5_abi_version(void);
+
+/* Number of HIP devices visible to this process (0 without a GPU); does not
+ * initialise the runtime. */
+QSMD5_API int qsmd5_device_count(void);
+
+/* Static text for an error code returned by this library. */
+QSMD5_API const char* qsmd5_strerror(int err);
+
+/* Detail of the last failure on the calling thread ("" if none). */
+QSMD5_API const char* qsmd5_last_error(void);
+
+/* md5(std::string) / md5(iostream) for one buffer (MD5.cpp:335-349).
+ * Synchronous. */
+QSMD5_API int qsmd5_hash_one(const void* ptr, uint64_t len, uint8_t digest[16]);
+
+/* Hash n independent chunks (qsfs upload parts) in one GPU batch.
+ * digests[i] receives the MD5 of chunks[i].  Synchronous: returns when every
+ * digest is in `digests` (host memory).  Host-resident chunks are copied to
+ * the GPU in slices that overlap with hashing. */
+QSMD5_API int qsmd5_hash_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16]);
+
+/* As qsmd5_hash_batch with QSMD5_FLAG_* flags. */
+QSMD5_API int qsmd5_hash_batch_ex(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags);
+
+/* Device-resident fast path, asynchronous on `hip_stream` (a hipStream_t, or
+ * NULL for the legacy default stream): d_chunks, d_order and d_digests are
+ * device memory, every chunk ptr is device memory.  d_order (optional, may be
+ * NULL) lists chunk indices in the order lanes take them; the host should pass
+ * lengths sorted descending so the lanes of a wavefront finish together.
+ * Only enqueues work; the caller synchronises the stream. */
+QSMD5_API int qsmd5_hash_batch_device_async(const qsmd5_chunk* d_chunks, const uint32_t* d_order, size_t n,
+                                  uint8_t (*d_digests)[16], void* hip_stream);
+
+/* Which kernel qsmd5_hash_batch_device_async launches for a batch of n
+ * chunks: 1 = producer/consumer latency kernel, 0 = one-wave throughput
+ * kernel.  QSMD5_KERNEL env ("pc"/"v1") overrides. */
+QSMD5_API int qsmd5_kernel_choice(size_t n);
+
+/* Lowercase hex, exactly MD5::hexdigest()'s "%02x" x 16 (MD5.cpp:317-325);
+ * out must hold 33 bytes (NUL-terminated).  Host-only, needs no GPU. */
+QSMD5_API void qsmd5_hex(const uint8_t digest[16], char out[33]);
+
+/* Streaming context: the reference MD5 class (update()* then finalize()). */
+typedef struct qsmd5_ctx qsmd5_ctx;
+QSMD5_API int qsmd5_ctx_create(qsmd5_ctx** out);
+QSMD5_API int qsmd5_ctx_update(qsmd5_ctx* ctx, const void* ptr, uint64_t len);
+QSMD5_API int qsmd5_ctx_final(qsmd5_ctx* ctx, uint8_t digest[16]);
+QSMD5_API void qsmd5_ctx_destroy(qsmd5_ctx* ctx);
+
+/* Pinned (page-locked) host buffers for the transfer-buffer pool
+ * (ResourceManager, src/data/ResourceManager.cpp:53-77): the page gather
+ * (File::ReadNoLoad) can fill them and the GPU reads them by DMA. */
+QSMD5_API int qsmd5_alloc_pinned(size_t bytes, void** out);
+QSMD5_API int qsmd5_free_pinned(void* ptr);
+
+/* Part slicing identical to QSTransferManager::PrepareUpload
+ * (QSTransferManager.cpp:492-546): a single part below `threshold`, else
+ * parts of `buf_size` with the last two averaged when the remainder is below
+ * `min_part`.  Offsets start at `range_begin`.  Writes up to `cap` parts and
+ * sets *nparts to the number needed (call with cap = 0 to size).
+ * Host-only, needs no GPU.  Reference defaults: buf 10 MiB, min 4 MiB,
+ * threshold 20 MiB (configure/Default.cpp:159-177). */
+QSMD5_API int qsmd5_plan_parts(uint64_t file_size, uint64_t buf_size, uint64_t min_part,
+                     uint64_t threshold, uint64_t range_begin, qsmd5_part* parts, size_t cap,
+                     size_t* nparts);
+
+/* Batch pre-hash of a whole file's parts in one call: digests[i] = MD5 of
+ * file[parts[i].offset - parts[0].offset ... + parts[i].size).  `file` points
+ * at the byte for parts[0].offset (host or device memory). */
+QSMD5_API int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t n, uint8_t (*digests)[16]);
+
+/* Timing of the most recent synchronous batch on this process (ms): total
+ * wall, and GPU kernel time between the first and last kernel event. */
+QSMD5_API int qsmd5_last_timing(double* wall_ms, double* kernel_ms);
+
+/* Test/bench support (synthetic data, not used by the hashing path): fill
+ * nchunks device chunks at base + i*stride with `len` bytes of the LCG of
+ * SURVEY.md §8c seeded with seed0 + i.  Asynchronous on hip_stream. */
+QSMD5_API int qsmd5_synth_fill_lcg(void* d_base, uint64_t stride, uint64_t len, uint32_t seed0,
+                         uint32_t nchunks, void* hip_stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* QSMD5_H_ */

@@ -1,0 +1,443 @@
+// qsfs-fuse_amd/csrc/md5_kernels.hip -- gfx950 kernels for the qsfs MD5 path.
+//
+// Kernels
+//   qsmd5_batch_kernel   one lane per chunk (qsfs upload part); hashes the
+//                        whole message incl. RFC 1321 padding and writes the
+//                        16-byte digest.  Replaces md5(shared_ptr<iostream>)
+//                        (reference src/base/MD5.cpp:341-349) for a batch.
+//   qsmd5_blocks_kernel  advances one streaming state over whole blocks
+//                        (the MD5 class's update(), MD5.cpp:240-269).
+//   qsmd5_lcg_fill_kernel synthetic-data generator (bench/tests only): the
+//                        LCG of SURVEY.md §8c, jump-ahead parallel.
+//
+// Why lane-per-chunk: MD5 is Merkle-Damgard, so a chunk is a strictly serial
+// chain of 64-byte compressions; parallelism exists only across chunks.  A
+// wave issues one instruction per ~4 cycles when alone on its SIMD, so the
+// per-chain rate is set by instructions per block, not by lanes per wave --
+// packing 64 chains into one wave costs nothing per chain and leaves the other
+// SIMDs free.  Workgroups are one wave each so the dispatcher spreads them
+// over all 8 XCDs / 256 CUs.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "md5_core.h"
+
+namespace qsmd5 {
+
+struct ChunkDesc {  // layout-identical to qsmd5_chunk in include/qsmd5.h
+  const uint8_t* ptr;
+  uint64_t len;
+};
+
+// Whole blocks from a 4-byte-aligned pointer.  Four blocks (64 VGPRs) are
+// kept in flight so the ~1-2 us HBM latency hides behind ~3 blocks of compute.
+// Prefetch addresses are clamped to the last block (always in bounds).
+__device__ __forceinline__ void blocks_aligned4(uint32_t (&st)[4], const uint32_t* p,
+                                                uint32_t nblk) {
+  if (nblk == 0) return;
+  const uint32_t last = nblk - 1;
+  u32x4 a0, a1, a2, a3, b0, b1, b2, b3, c0, c1, c2, c3, d0, d1, d2, d3;
+#define QS_LOAD(X, blk)                                   \
+  do {                                                    \
+    const uint32_t* q_ = p + (uint64_t)(blk) * 16u;       \
+    X##0 = load16_a4(q_);                                 \
+    X##1 = load16_a4(q_ + 4);                             \
+    X##2 = load16_a4(q_ + 8);                             \
+    X##3 = load16_a4(q_ + 12);                            \
+  } while (0)
+#define QS_COMPRESS(X)            \
+  do {                            \
+    uint32_t w_[16];              \
+    unpack4(w_, 0, X##0);         \
+    unpack4(w_, 1, X##1);         \
+    unpack4(w_, 2, X##2);         \
+    unpack4(w_, 3, X##3);         \
+    md5_compress(st, w_);         \
+  } while (0)
+  QS_LOAD(a, 0);
+  QS_LOAD(b, min(1u, last));
+  QS_LOAD(c, min(2u, last));
+  QS_LOAD(d, min(3u, last));
+  uint32_t j = 0;
+  for (; j + 4 <= nblk; j += 4) {
+    QS_COMPRESS(a);
+    QS_LOAD(a, min(j + 4, last));
+    QS_COMPRESS(b);
+    QS_LOAD(b, min(j + 5, last));
+    QS_COMPRESS(c);
+    QS_LOAD(c, min(j + 6, last));
+    QS_COMPRESS(d);
+    QS_LOAD(d, min(j + 7, last));
+  }
+  if (j < nblk) QS_COMPRESS(a);
+  if (j + 1 < nblk) QS_COMPRESS(b);
+  if (j + 2 < nblk) QS_COMPRESS(c);
+#undef QS_COMPRESS
+#undef QS_LOAD
+}
+
+// Whole blocks from an arbitrary byte address: aligned dword window of 17
+// words per block, realigned with v_alignbyte_b32.  Every dword read holds at
+// least one byte of the message, so nothing past the buffer's last aligned
+// dword is touched.
+__device__ __forceinline__ void blocks_unaligned(uint32_t (&st)[4], const uint8_t* bp,
+                                                 uint32_t nblk) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(bp);
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const uint32_t off = static_cast<uint32_t>(a & 3u);
+  for (uint32_t j = 0; j < nblk; ++j) {
+    const uint32_t* q = base + (uint64_t)j * 16u;
+    u32x4 x0 = load16_a4(q), x1 = load16_a4(q + 4), x2 = load16_a4(q + 8),
+          x3 = load16_a4(q + 12);
+    uint32_t e = load4(q + 16);
+    uint32_t d[17] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w, x2.x,
+                      x2.y, x2.z, x2.w, x3.x, x3.y, x3.z, x3.w, e};
+    uint32_t w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], off);
+    md5_compress(st, w);
+  }
+}
+
+// Final 1 or 2 blocks: the rem (< 64) trailing bytes, 0x80, zero fill, and the
+// 64-bit little-endian bit count (MD5.cpp:282-312).
+__device__ __forceinline__ void finish(uint32_t (&st)[4], const uint8_t* tp, uint32_t rem,
+                                       uint64_t total_len) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(tp);
+  const uint32_t* base = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const uint32_t off = static_cast<uint32_t>(a & 3u);
+  uint32_t d[17];
+#pragma unroll
+  for (int k = 0; k < 17; ++k) d[k] = (uint32_t)(4 * k) < off + rem ? load4(base + k) : 0u;
+  uint32_t w[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    uint32_t x = __builtin_amdgcn_alignbyte(d[k + 1], d[k], off);
+    const uint32_t lo = 4u * k;
+    uint32_t m = rem >= lo + 4u ? 0xffffffffu : rem <= lo ? 0u : ((1u << (8u * (rem - lo))) - 1u);
+    x &= m;
+    if ((rem >> 2) == (uint32_t)k) x |= 0x80u << (8u * (rem & 3u));
+    w[k] = x;
+  }
+  const uint64_t bits = total_len << 3;
+  if (rem < 56u) {
+    w[14] = (uint32_t)bits;
+    w[15] = (uint32_t)(bits >> 32);
+    md5_compress(st, w);
+  } else {
+    md5_compress(st, w);
+#pragma unroll
+    for (int k = 0; k < 14; ++k) w[k] = 0u;
+    w[14] = (uint32_t)bits;
+    w[15] = (uint32_t)(bits >> 32);
+    md5_compress(st, w);
+  }
+}
+
+__device__ __forceinline__ void hash_message(uint32_t (&st)[4], const uint8_t* p, uint64_t len) {
+  const uint32_t nblk = (uint32_t)(len >> 6);
+  if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0)
+    blocks_aligned4(st, reinterpret_cast<const uint32_t*>(p), nblk);
+  else
+    blocks_unaligned(st, p, nblk);
+  finish(st, p + ((uint64_t)nblk << 6), (uint32_t)(len & 63u), len);
+}
+
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
+// LDS-only workgroup barrier: wait for this wave's LDS traffic, then s_barrier.
+// Deliberately not __syncthreads(): its fence would also drain vmcnt and kill
+// the producer's global-load prefetch that spans the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// ---- producer/consumer batch kernel -------------------------------------------
+// Workgroup = 2 waves over the same 64 chunks.  Wave 1 (producer) streams the
+// message blocks from HBM, realigns them, and writes mk[i] = x[word(i)] + K[i]
+// for all 64 steps of each block into an LDS ring; wave 0 (chain) runs only the
+// serial part: 4 VALU per step plus one ds_read_b128 per 4 steps.  The two waves
+// sit on different SIMDs, so the chain wave's issue slots are not shared.
+constexpr int kPcHalf = 4;                   // blocks per ring half (one phase)
+constexpr int kPcSlots = 2 * kPcHalf;        // 8 x 16 KiB = 128 KiB of LDS
+
+struct PcBlockRegs {
+  u32x4 q[4];
+  uint32_t e;
+};
+
+__device__ __forceinline__ void pc_load_block(PcBlockRegs& r, const uint32_t* base, uint32_t off,
+                                              uint32_t blk) {
+  const uint32_t* q = base + (uint64_t)blk * 16u;
+  r.q[0] = load16_a4(q);
+  r.q[1] = load16_a4(q + 4);
+  r.q[2] = load16_a4(q + 8);
+  r.q[3] = load16_a4(q + 12);
+  r.e = off ? load4(q + 16) : 0u;  // 17th dword holds message bytes only if off != 0
+}
+
+__device__ __forceinline__ void pc_write_mk(u32x4 (*slot)[64], uint32_t lane, const PcBlockRegs& r,
+                                            uint32_t off) {
+  uint32_t d[17] = {r.q[0].x, r.q[0].y, r.q[0].z, r.q[0].w, r.q[1].x, r.q[1].y,
+                    r.q[1].z, r.q[1].w, r.q[2].x, r.q[2].y, r.q[2].z, r.q[2].w,
+                    r.q[3].x, r.q[3].y, r.q[3].z, r.q[3].w, r.e};
+  uint32_t w[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], off);
+#pragma unroll
+  for (int g = 0; g < 16; ++g) {
+    u32x4 m;
+    m.x = w[md5_word(4 * g + 0)] + Md5Tables::K[4 * g + 0];
+    m.y = w[md5_word(4 * g + 1)] + Md5Tables::K[4 * g + 1];
+    m.z = w[md5_word(4 * g + 2)] + Md5Tables::K[4 * g + 2];
+    m.w = w[md5_word(4 * g + 3)] + Md5Tables::K[4 * g + 3];
+    slot[g][lane] = m;
+  }
+}
+
+}  // namespace qsmd5
+
+using namespace qsmd5;
+
+// digests: n x 16 bytes (4 LE words each), indexed by chunk index.
+// order: optional lane -> chunk permutation (length-bucketed by the host).
+extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_kernel(
+    const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
+    uint32_t* __restrict__ digests) {
+  const uint32_t t = blockIdx.x * 64u + threadIdx.x;
+  if (t >= n) return;
+  const uint32_t idx = order ? order[t] : t;
+  const ChunkDesc cd = chunks[idx];
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  hash_message(st, cd.ptr, cd.len);
+  u32x4 o = {st[0], st[1], st[2], st[3]};
+  *reinterpret_cast<u32x4*>(digests + 4u * (uint64_t)idx) = o;
+}
+
+// Streaming update: state[4] advanced over nblk whole blocks at p.
+extern "C" __global__ __launch_bounds__(64) void qsmd5_blocks_kernel(uint32_t* __restrict__ state,
+                                                                     const uint8_t* p,
+                                                                     uint32_t nblk) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t st[4] = {state[0], state[1], state[2], state[3]};
+  if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0)
+    blocks_aligned4(st, reinterpret_cast<const uint32_t*>(p), nblk);
+  else
+    blocks_unaligned(st, p, nblk);
+  state[0] = st[0];
+  state[1] = st[1];
+  state[2] = st[2];
+  state[3] = st[3];
+}
+
+// Streaming finalize: tail bytes (< 64, host-provided in device memory) + pad.
+extern "C" __global__ __launch_bounds__(64) void qsmd5_final_kernel(uint32_t* __restrict__ state,
+                                                                    const uint8_t* tail,
+                                                                    uint32_t rem,
+                                                                    uint64_t total_len) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint32_t st[4] = {state[0], state[1], state[2], state[3]};
+  finish(st, tail, rem, total_len);
+  state[0] = st[0];
+  state[1] = st[1];
+  state[2] = st[2];
+  state[3] = st[3];
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic data: chunk i of `nchunks` at base + i*stride holds `len` bytes of
+// LCG(seed0 + i): x <- x*1103515245 + 12345 before each byte, byte = x>>16.
+// Each thread writes one 1 KiB segment after jumping the LCG ahead.
+namespace {
+constexpr uint32_t kLcgA = 1103515245u;
+constexpr uint32_t kLcgC = 12345u;
+constexpr uint32_t kSeg = 1024u;
+
+__device__ __forceinline__ uint32_t lcg_jump(uint32_t x, uint64_t n) {
+  uint32_t am = kLcgA, cm = kLcgC;  // T^(2^k)
+  uint32_t ar = 1u, cr = 0u;        // accumulated map
+  while (n) {
+    if (n & 1u) {
+      ar = ar * am;
+      cr = cr * am + cm;
+    }
+    cm = cm * am + cm;
+    am = am * am;
+    n >>= 1;
+  }
+  return ar * x + cr;
+}
+}  // namespace
+
+extern "C" __global__ __launch_bounds__(256) void qsmd5_lcg_fill_kernel(
+    uint8_t* __restrict__ base, uint64_t stride, uint64_t len, uint32_t seed0,
+    uint32_t nchunks, uint64_t segs_per_chunk) {
+  const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t chunk = g / segs_per_chunk;
+  if (chunk >= nchunks) return;
+  const uint64_t seg = g - chunk * segs_per_chunk;
+  const uint64_t start = seg * kSeg;
+  if (start >= len) return;
+  const uint64_t end = start + kSeg < len ? start + kSeg : len;
+  uint32_t x = lcg_jump(seed0 + (uint32_t)chunk, start);
+  uint8_t* out = base + chunk * stride;
+  uint64_t i = start;
+  if (((reinterpret_cast<uintptr_t>(out) + start) & 3u) == 0) {
+    for (; i + 4 <= end; i += 4) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        x = x * kLcgA + kLcgC;
+        v |= ((x >> 16) & 0xffu) << (8 * b);
+      }
+      *reinterpret_cast<uint32_t*>(out + i) = v;
+    }
+  }
+  for (; i < end; ++i) {
+    x = x * kLcgA + kLcgC;
+    out[i] = (uint8_t)(x >> 16);
+  }
+}
+
+// Latency-regime batch kernel (B up to ~64 K chunks): see qsmd5::kPcHalf notes.
+extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
+    const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
+    uint32_t* __restrict__ digests) {
+  __shared__ u32x4 ring[kPcSlots][16][64];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t t = blockIdx.x * 64u + lane;
+  uint32_t idx = 0;
+  ChunkDesc cd = {nullptr, 0};
+  if (t < n) {
+    idx = order ? order[t] : t;
+    cd = chunks[idx];
+  }
+  const uint32_t nblk = (uint32_t)(cd.len >> 6);
+  const uint32_t phases = (wave_max_u32(nblk) + kPcHalf - 1) / kPcHalf;
+  const uintptr_t pa = reinterpret_cast<uintptr_t>(cd.ptr);
+  const uint32_t off = (uint32_t)(pa & 3u);
+
+  if (wave == 1) {
+    // ---------------- producer ----------------
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(pa & ~uintptr_t(3));
+    const uint32_t last = nblk ? nblk - 1 : 0;
+    PcBlockRegs r[kPcHalf];
+    auto load_phase = [&](uint32_t p) {
+      if (nblk) {
+#pragma unroll
+        for (int h = 0; h < kPcHalf; ++h) pc_load_block(r[h], base, off, min(p * kPcHalf + h, last));
+      }
+    };
+    auto write_phase = [&](uint32_t p) {
+      if (nblk) {
+#pragma unroll
+        for (int h = 0; h < kPcHalf; ++h)
+          pc_write_mk(ring[(p & 1u) * kPcHalf + h], lane, r[h], off);
+      }
+    };
+    if (phases > 0) {
+      load_phase(0);
+      write_phase(0);
+      load_phase(1);
+    }
+    lds_barrier();
+    for (uint32_t p = 0; p < phases; ++p) {
+      if (p + 1 < phases) {
+        write_phase(p + 1);
+        load_phase(p + 2);
+      }
+      lds_barrier();
+    }
+    return;
+  }
+
+  // ---------------- chain ----------------
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  lds_barrier();
+  for (uint32_t p = 0; p < phases; ++p) {
+    const uint32_t s0 = (p & 1u) * kPcHalf;
+    u32x4 cur[16];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) cur[g] = ring[s0][g][lane];
+#pragma unroll
+    for (int h = 0; h < kPcHalf; ++h) {
+      u32x4 nxt[16];
+      if (h + 1 < kPcHalf) {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) nxt[g] = ring[s0 + h + 1][g][lane];
+      }
+      if (p * kPcHalf + h < nblk) {
+        uint32_t mk[64];
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          mk[4 * g + 0] = cur[g].x;
+          mk[4 * g + 1] = cur[g].y;
+          mk[4 * g + 2] = cur[g].z;
+          mk[4 * g + 3] = cur[g].w;
+        }
+        md5_compress_mk(st, mk);
+      }
+      if (h + 1 < kPcHalf) {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) cur[g] = nxt[g];
+      }
+    }
+    lds_barrier();
+  }
+  if (t >= n) return;
+  finish(st, cd.ptr + ((uint64_t)nblk << 6), (uint32_t)(cd.len & 63u), cd.len);
+  u32x4 o = {st[0], st[1], st[2], st[3]};
+  *reinterpret_cast<u32x4*>(digests + 4u * (uint64_t)idx) = o;
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers (md5_launch.h).
+#include "md5_launch.h"
+
+namespace qsmd5 {
+
+hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
+                        int kind, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t groups = (n + 63u) / 64u;
+  if (kind == kKernelLatency) {
+    hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(groups), dim3(128), 0, s,
+                       static_cast<const ChunkDesc*>(chunks), order, n, digests);
+  } else {
+    hipLaunchKernelGGL(qsmd5_batch_kernel, dim3(groups), dim3(64), 0, s,
+                       static_cast<const ChunkDesc*>(chunks), order, n, digests);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_blocks(uint32_t* state, const uint8_t* p, uint32_t nblk, hipStream_t s) {
+  if (nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(qsmd5_blocks_kernel, dim3(1), dim3(64), 0, s, state, p, nblk);
+  return hipGetLastError();
+}
+
+hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint64_t total_len,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(qsmd5_final_kernel, dim3(1), dim3(64), 0, s, state, tail, rem, total_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_lcg_fill(uint8_t* base, uint64_t stride, uint64_t len, uint32_t seed0,
+                           uint32_t nchunks, hipStream_t s) {
+  if (nchunks == 0 || len == 0) return hipSuccess;
+  const uint64_t segs = (len + kSeg - 1) / kSeg;
+  const uint64_t threads = segs * nchunks;
+  const uint64_t blocks = (threads + 255) / 256;
+  if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(qsmd5_lcg_fill_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, base, stride,
+                     len, seed0, nchunks, segs);
+  return hipGetLastError();
+}
+
+}  // namespace qsmd5

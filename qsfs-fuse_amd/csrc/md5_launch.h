@@ -1,0 +1,29 @@
+// qsfs-fuse_amd/csrc/md5_launch.h -- host-side launchers for md5_kernels.hip
+// (private to libqsmd5; the public surface is include/qsmd5.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace qsmd5 {
+
+enum KernelKind : int {
+  kKernelThroughput = 0,  // qsmd5_batch_kernel: 1 wave / 64 chunks, all work in-wave
+  kKernelLatency = 1,     // qsmd5_batch_pc_kernel: producer + chain wave / 64 chunks
+};
+
+// Chunks one launch of the latency kernel keeps resident at once: one
+// 128 KiB-LDS workgroup per CU, 64 chunks each.
+constexpr uint32_t kLatencyKernelResident = 256u * 64u;
+
+// chunks: device array of {ptr,len}; order: optional device lane->chunk map;
+// digests: device, 16 B per chunk indexed by chunk index.
+hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
+                        int kind, hipStream_t s);
+hipError_t launch_blocks(uint32_t* state, const uint8_t* p, uint32_t nblk, hipStream_t s);
+hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint64_t total_len,
+                        hipStream_t s);
+hipError_t launch_lcg_fill(uint8_t* base, uint64_t stride, uint64_t len, uint32_t seed0,
+                           uint32_t nchunks, hipStream_t s);
+
+}  // namespace qsmd5

@@ -1,0 +1,724 @@
+// qsfs-fuse_amd/csrc/qsmd5_runtime.cpp -- host runtime behind include/qsmd5.h.
+//
+// Owns the device, streams, descriptor/digest scratch and the host->device
+// staging ring.  Every entry point is extern "C", catches everything, and
+// reports failure as a negative errno (never an empty digest).  There is no
+// CPU hashing path: the only MD5 implementation in this library is the gfx950
+// kernel set in md5_kernels.hip.
+//
+// Host-resident batches (the qsfs case: parts sit in pooled host buffers,
+// ResourceManager.cpp:53-77) are cut into slices of about kSliceBytes; each
+// slice is copied H2D into a ring region on the copy stream and hashed by its
+// own launch on one of kComputeStreams streams, so PCIe transfer of slice k+1
+// overlaps hashing of slice k and slice kernels run concurrently (each one is
+// latency-bound on a handful of CUs).
+#include <errno.h>
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <mutex>
+#include <new>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/qsmd5.h"
+#include "md5_launch.h"
+
+namespace {
+
+using qsmd5::kKernelLatency;
+using qsmd5::kKernelThroughput;
+
+constexpr uint64_t kMaxChunkLen = 1ull << 38;
+constexpr int kComputeStreams = 8;
+constexpr uint64_t kSliceBytes = 1ull << 30;        // ~1 GiB per H2D slice
+constexpr uint64_t kDefaultStaging = 16ull << 30;   // device staging ring
+constexpr uint64_t kAlign = 256;
+
+thread_local std::string t_last_error;
+
+int fail(int code, const std::string& what) {
+  t_last_error = what;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  std::string s = std::string(what) + ": " + hipGetErrorString(e);
+  return fail(e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? -ENOMEM : -EIO, s);
+}
+
+#define QS_HIP(call)                                  \
+  do {                                                \
+    hipError_t e_ = (call);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #call); \
+  } while (0)
+
+uint64_t env_u64(const char* name, uint64_t dflt) {
+  const char* v = getenv(name);
+  if (!v || !*v) return dflt;
+  char* end = nullptr;
+  unsigned long long x = strtoull(v, &end, 0);
+  return (end && *end == 0) ? (uint64_t)x : dflt;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) {
+      (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return hip_fail(e, "hipMalloc");
+    }
+    cap = want;
+    return 0;
+  }
+};
+
+struct HostPinned {
+  void* p = nullptr;
+  size_t cap = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= cap) return 0;
+    if (p) {
+      (void)hipHostFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+    size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return hip_fail(e, "hipHostMalloc");
+    }
+    cap = want;
+    return 0;
+  }
+};
+
+struct Runtime {
+  std::mutex mu;  // serialises batches on the device
+  bool ready = false;
+  int init_rc = 0;
+  int device = -1;
+  hipStream_t copy = nullptr;
+  hipStream_t compute[kComputeStreams] = {};
+  DevBuf d_desc, d_order, d_dig, d_staging;
+  HostPinned h_desc, h_order, h_dig;
+  uint64_t staging_cap = kDefaultStaging;
+  double last_wall_ms = 0, last_kernel_ms = 0;
+};
+
+Runtime& rt() {
+  static Runtime* r = new Runtime;  // intentionally leaked: no teardown order issues
+  return *r;
+}
+
+std::once_flag g_init_once;
+
+void do_init() {
+  Runtime& r = rt();
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) {
+    r.init_rc = fail(-ENODEV, "qsmd5: no usable GPU (hipGetDeviceCount)");
+    return;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const char* ed = getenv("QSMD5_DEVICE");
+  if (ed && *ed) dev = atoi(ed);
+  if (dev < 0 || dev >= n) {
+    r.init_rc = fail(-ENODEV, "qsmd5: QSMD5_DEVICE out of range");
+    return;
+  }
+  if ((e = hipSetDevice(dev)) != hipSuccess) {
+    r.init_rc = hip_fail(e, "hipSetDevice");
+    return;
+  }
+  if ((e = hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking)) != hipSuccess) {
+    r.init_rc = hip_fail(e, "hipStreamCreate");
+    return;
+  }
+  for (auto& s : r.compute) {
+    if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) {
+      r.init_rc = hip_fail(e, "hipStreamCreate");
+      return;
+    }
+  }
+  r.staging_cap = env_u64("QSMD5_STAGING_BYTES", kDefaultStaging);
+  r.device = dev;
+  r.ready = true;
+  r.init_rc = 0;
+}
+
+int ensure_init() {
+  std::call_once(g_init_once, do_init);
+  Runtime& r = rt();
+  if (!r.ready) return r.init_rc ? r.init_rc : -ENODEV;
+  // Calls may come from threads whose current device differs.
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != r.device) {
+    hipError_t e = hipSetDevice(r.device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  }
+  return 0;
+}
+
+enum MemKind { kHostMem = 0, kDeviceMem = 1 };
+
+MemKind classify(const void* p) {
+  if (!p) return kHostMem;
+  hipPointerAttribute_t a;
+  memset(&a, 0, sizeof(a));
+  hipError_t e = hipPointerGetAttributes(&a, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // pageable host memory: clear the sticky error
+    return kHostMem;
+  }
+  return a.type == hipMemoryTypeDevice ? kDeviceMem : kHostMem;
+}
+
+int kernel_choice(size_t n) {
+  const char* k = getenv("QSMD5_KERNEL");
+  if (k && !strcmp(k, "pc")) return kKernelLatency;
+  if (k && !strcmp(k, "v1")) return kKernelThroughput;
+  // The latency kernel wins while every chunk has its own chain lane in one
+  // resident round; beyond that the one-wave kernel's 2 waves/SIMD win.
+  return n <= qsmd5::kLatencyKernelResident ? kKernelLatency : kKernelThroughput;
+}
+
+struct Slice {
+  size_t first, count;  // range in the host-chunk order list
+  uint64_t bytes;
+};
+
+// The synchronous batch: device chunks in one launch; host chunks sliced,
+// staged and hashed with copy/compute overlap.  Caller holds rt().mu.
+int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
+  Runtime& r = rt();
+  auto t0 = std::chrono::steady_clock::now();
+  if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
+
+  std::vector<uint64_t> len(n);
+  std::vector<MemKind> kind(n);
+  uint64_t max_host = 0, host_total = 0;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t L = chunks[i].len;
+    if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;
+    if (L >= kMaxChunkLen) return fail(-EINVAL, "qsmd5: chunk longer than 2^38 bytes");
+    if (L > 0 && !chunks[i].ptr) return fail(-EINVAL, "qsmd5: NULL ptr with non-zero len");
+    len[i] = L;
+    kind[i] = L ? classify(chunks[i].ptr) : kDeviceMem;  // empty chunks read nothing
+    if (kind[i] == kHostMem) {
+      max_host = std::max(max_host, L);
+      host_total += (L + kAlign - 1) & ~(kAlign - 1);
+    }
+  }
+
+  // Lane order: device chunks first, then host chunks; each group sorted by
+  // length (descending) so the lanes of a wavefront finish together.
+  std::vector<uint32_t> dev_idx, host_idx;
+  for (size_t i = 0; i < n; ++i) (kind[i] == kDeviceMem ? dev_idx : host_idx).push_back((uint32_t)i);
+  auto by_len = [&](uint32_t a, uint32_t b) { return len[a] > len[b] || (len[a] == len[b] && a < b); };
+  std::sort(dev_idx.begin(), dev_idx.end(), by_len);
+  std::sort(host_idx.begin(), host_idx.end(), by_len);
+
+  // Slices of host chunks and their staging regions.
+  const uint64_t region = std::max<uint64_t>(kSliceBytes, (max_host + kAlign - 1) & ~(kAlign - 1));
+  std::vector<Slice> slices;
+  for (size_t k = 0; k < host_idx.size();) {
+    Slice s{k, 0, 0};
+    while (k < host_idx.size()) {
+      uint64_t L = (len[host_idx[k]] + kAlign - 1) & ~(kAlign - 1);
+      if (s.count > 0 && s.bytes + L > region) break;
+      s.bytes += L;
+      ++s.count;
+      ++k;
+    }
+    slices.push_back(s);
+  }
+  size_t nregions = 0;
+  if (!slices.empty()) {
+    uint64_t cap = std::min<uint64_t>(r.staging_cap, host_total + region);
+    nregions = (size_t)std::max<uint64_t>(1, cap / region);
+    nregions = std::min(nregions, slices.size());
+    if (int rc = r.d_staging.reserve(nregions * region)) return rc;
+  }
+
+  // Descriptors (device pointers) for every chunk, upfront.
+  if (int rc = r.h_desc.reserve(n * sizeof(qsmd5_chunk) + 16)) return rc;
+  if (int rc = r.h_order.reserve(n * sizeof(uint32_t) + 16)) return rc;
+  if (int rc = r.h_dig.reserve(n * 16 + 16)) return rc;
+  if (int rc = r.d_desc.reserve(n * sizeof(qsmd5_chunk) + 16)) return rc;
+  if (int rc = r.d_order.reserve(n * sizeof(uint32_t) + 16)) return rc;
+  if (int rc = r.d_dig.reserve(n * 16 + 16)) return rc;
+  qsmd5_chunk* hd = static_cast<qsmd5_chunk*>(r.h_desc.p);
+  uint32_t* ho = static_cast<uint32_t*>(r.h_order.p);
+  for (size_t i = 0; i < n; ++i) hd[i] = {chunks[i].ptr, len[i]};
+  uint8_t* stage = static_cast<uint8_t*>(r.d_staging.p);
+  std::vector<std::vector<uint64_t>> stage_off(slices.size());
+  for (size_t si = 0; si < slices.size(); ++si) {
+    uint8_t* base = stage + (si % nregions) * region;
+    uint64_t off = 0;
+    for (size_t k = 0; k < slices[si].count; ++k) {
+      uint32_t ci = host_idx[slices[si].first + k];
+      hd[ci].ptr = base + off;
+      stage_off[si].push_back(off);
+      off += (len[ci] + kAlign - 1) & ~(kAlign - 1);
+    }
+  }
+  size_t pos = 0;
+  for (uint32_t ci : dev_idx) ho[pos++] = ci;
+  for (uint32_t ci : host_idx) ho[pos++] = ci;
+
+  hipStream_t s0 = r.compute[0];
+  QS_HIP(hipMemcpyAsync(r.d_desc.p, hd, n * sizeof(qsmd5_chunk), hipMemcpyHostToDevice, s0));
+  QS_HIP(hipMemcpyAsync(r.d_order.p, ho, n * sizeof(uint32_t), hipMemcpyHostToDevice, s0));
+  hipEvent_t meta_ready, k_first = nullptr, k_last = nullptr;
+  QS_HIP(hipEventCreateWithFlags(&meta_ready, hipEventDisableTiming));
+  QS_HIP(hipEventRecord(meta_ready, s0));
+  QS_HIP(hipEventCreate(&k_first));
+  QS_HIP(hipEventCreate(&k_last));
+  std::vector<hipEvent_t> region_free(nregions, nullptr);
+  std::vector<hipEvent_t> to_destroy;
+  int rc = 0;
+  auto cleanup = [&]() {
+    (void)hipEventDestroy(meta_ready);
+    for (hipEvent_t e : to_destroy) (void)hipEventDestroy(e);
+  };
+  const uint32_t* d_order = static_cast<const uint32_t*>(r.d_order.p);
+  uint32_t* d_dig = static_cast<uint32_t*>(r.d_dig.p);
+  bool first_kernel = true;
+  auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt) -> int {
+    if (first_kernel) {
+      QS_HIP(hipEventRecord(k_first, s));
+      first_kernel = false;
+    }
+    hipError_t e = qsmd5::launch_batch(r.d_desc.p, ord, (uint32_t)cnt, d_dig, kernel_choice(cnt), s);
+    if (e != hipSuccess) return hip_fail(e, "qsmd5 kernel launch");
+    return 0;
+  };
+
+  // Device-resident chunks: one launch.
+  if (!dev_idx.empty()) {
+    if ((rc = launch(s0, d_order, dev_idx.size()))) {
+      cleanup();
+      return rc;
+    }
+  }
+  // Host-resident slices.
+  for (size_t si = 0; si < slices.size() && rc == 0; ++si) {
+    const size_t reg = si % nregions;
+    hipStream_t cs = r.compute[1 + si % (kComputeStreams - 1)];
+    if (region_free[reg]) {
+      hipError_t e = hipStreamWaitEvent(r.copy, region_free[reg], 0);
+      if (e != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
+    }
+    for (size_t k = 0; k < slices[si].count && rc == 0; ++k) {
+      uint32_t ci = host_idx[slices[si].first + k];
+      if (len[ci] == 0) continue;
+      hipError_t e = hipMemcpyAsync(const_cast<void*>(hd[ci].ptr), chunks[ci].ptr, len[ci],
+                                    hipMemcpyHostToDevice, r.copy);
+      if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync H2D");
+    }
+    if (rc) break;
+    hipEvent_t copied;
+    if (hipEventCreateWithFlags(&copied, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(copied, r.copy) != hipSuccess) {
+      rc = fail(-EIO, "qsmd5: event record failed");
+      break;
+    }
+    to_destroy.push_back(copied);
+    if (hipStreamWaitEvent(cs, copied, 0) != hipSuccess ||
+        hipStreamWaitEvent(cs, meta_ready, 0) != hipSuccess) {
+      rc = fail(-EIO, "qsmd5: stream wait failed");
+      break;
+    }
+    if ((rc = launch(cs, d_order + dev_idx.size() + slices[si].first, slices[si].count))) break;
+    hipEvent_t done;
+    if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(done, cs) != hipSuccess) {
+      rc = fail(-EIO, "qsmd5: event record failed");
+      break;
+    }
+    to_destroy.push_back(done);
+    region_free[reg] = done;
+  }
+  if (rc) {
+    (void)hipDeviceSynchronize();
+    cleanup();
+    return rc;
+  }
+  // Join every compute stream into s0, then fetch digests.
+  for (int k = 1; k < kComputeStreams; ++k) {
+    hipEvent_t j;
+    if (hipEventCreateWithFlags(&j, hipEventDisableTiming) != hipSuccess) {
+      rc = fail(-EIO, "qsmd5: event create failed");
+      break;
+    }
+    to_destroy.push_back(j);
+    if (hipEventRecord(j, r.compute[k]) != hipSuccess || hipStreamWaitEvent(s0, j, 0) != hipSuccess) {
+      rc = fail(-EIO, "qsmd5: stream join failed");
+      break;
+    }
+  }
+  if (rc == 0 && !first_kernel) {
+    hipError_t e = hipEventRecord(k_last, s0);
+    if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
+  }
+  if (rc == 0) {
+    hipError_t e = hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0);
+    if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync D2H");
+  }
+  if (rc == 0) {
+    hipError_t e = hipStreamSynchronize(s0);
+    if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+  }
+  if (rc == 0) {
+    memcpy(digests, r.h_dig.p, n * 16);
+    float kms = 0;
+    if (!first_kernel && hipEventElapsedTime(&kms, k_first, k_last) == hipSuccess)
+      r.last_kernel_ms = kms;
+    else
+      r.last_kernel_ms = 0;
+    r.last_wall_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
+  (void)hipEventDestroy(k_first);
+  (void)hipEventDestroy(k_last);
+  cleanup();
+  return rc;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return fail(-ENOMEM, "qsmd5: host allocation failed");
+  } catch (...) {
+    return fail(-EIO, "qsmd5: internal error");
+  }
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------------------
+// Streaming context (MD5 class): state stays on the device between updates;
+// bytes that do not fill a 64-byte block wait in `tail` on the host
+// (MD5::buffer, MD5.h:79).
+struct qsmd5_ctx {
+  uint32_t* d_state = nullptr;  // 4 words
+  uint8_t* d_tail = nullptr;    // 64 bytes
+  uint8_t* d_stage = nullptr;   // staging for host updates
+  size_t stage_cap = 0;
+  uint8_t tail[64];
+  uint32_t tail_len = 0;
+  uint64_t total = 0;
+  bool finalized = false;
+  uint8_t digest[16];
+};
+
+extern "C" {
+
+int qsmd5_init(int flags) {
+  (void)flags;
+  return guarded([] { return ensure_init(); });
+}
+
+int qsmd5_abi_version(void) { return QSMD5_ABI_VERSION; }
+
+int qsmd5_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+const char* qsmd5_strerror(int err) {
+  switch (err) {
+    case 0: return "success";
+    case -EINVAL: return "invalid argument";
+    case -ENODEV: return "no usable GPU";
+    case -ENOMEM: return "out of memory";
+    case -EIO: return "GPU runtime error";
+    default: return "unknown error";
+  }
+}
+
+const char* qsmd5_last_error(void) { return t_last_error.c_str(); }
+
+void qsmd5_hex(const uint8_t digest[16], char out[33]) {
+  static const char kHex[] = "0123456789abcdef";
+  for (int i = 0; i < 16; ++i) {
+    out[2 * i] = kHex[digest[i] >> 4];
+    out[2 * i + 1] = kHex[digest[i] & 15];
+  }
+  out[32] = 0;
+}
+
+int qsmd5_hash_batch_ex(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
+  return guarded([&] {
+    if (n == 0) return 0;
+    if (!chunks || !digests) return fail(-EINVAL, "qsmd5: NULL chunks/digests");
+    if (int rc = ensure_init()) return rc;
+    std::lock_guard<std::mutex> lk(rt().mu);
+    return run_batch(chunks, n, digests, flags);
+  });
+}
+
+int qsmd5_hash_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16]) {
+  return qsmd5_hash_batch_ex(chunks, n, digests, 0);
+}
+
+int qsmd5_hash_one(const void* ptr, uint64_t len, uint8_t digest[16]) {
+  if (!digest) return fail(-EINVAL, "qsmd5: NULL digest");
+  qsmd5_chunk c = {ptr, len};
+  return qsmd5_hash_batch_ex(&c, 1, reinterpret_cast<uint8_t(*)[16]>(digest), 0);
+}
+
+int qsmd5_kernel_choice(size_t n) { return kernel_choice(n); }
+
+int qsmd5_hash_batch_device_async(const qsmd5_chunk* d_chunks, const uint32_t* d_order, size_t n,
+                                  uint8_t (*d_digests)[16], void* hip_stream) {
+  return guarded([&] {
+    if (n == 0) return 0;
+    if (!d_chunks || !d_digests) return fail(-EINVAL, "qsmd5: NULL device arrays");
+    if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
+    if (int rc = ensure_init()) return rc;
+    hipError_t e = qsmd5::launch_batch(d_chunks, d_order, (uint32_t)n,
+                                       reinterpret_cast<uint32_t*>(d_digests), kernel_choice(n),
+                                       static_cast<hipStream_t>(hip_stream));
+    if (e != hipSuccess) return hip_fail(e, "qsmd5 kernel launch");
+    return 0;
+  });
+}
+
+int qsmd5_alloc_pinned(size_t bytes, void** out) {
+  return guarded([&] {
+    if (!out) return fail(-EINVAL, "qsmd5: NULL out");
+    *out = nullptr;
+    if (int rc = ensure_init()) return rc;
+    QS_HIP(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    return 0;
+  });
+}
+
+int qsmd5_free_pinned(void* ptr) {
+  return guarded([&] {
+    if (!ptr) return 0;
+    if (int rc = ensure_init()) return rc;
+    QS_HIP(hipHostFree(ptr));
+    return 0;
+  });
+}
+
+int qsmd5_plan_parts(uint64_t file_size, uint64_t buf_size, uint64_t min_part, uint64_t threshold,
+                     uint64_t range_begin, qsmd5_part* parts, size_t cap, size_t* nparts) {
+  if (!nparts) return fail(-EINVAL, "qsmd5: NULL nparts");
+  if (buf_size == 0) return fail(-EINVAL, "qsmd5: buffer size must be > 0");
+  std::vector<qsmd5_part> v;
+  auto add = [&](uint64_t id, uint64_t off, uint64_t sz) {
+    qsmd5_part p;
+    p.part_number = (uint32_t)id;
+    p.reserved = 0;
+    p.offset = range_begin + off;
+    p.size = sz;
+    v.push_back(p);
+  };
+  try {
+    if (file_size < threshold) {
+      add(1, 0, file_size);  // single PutObject (QSTransferManager.cpp:543-546)
+    } else {
+      const uint64_t count = file_size / buf_size + (file_size % buf_size ? 1 : 0);
+      const uint64_t last = file_size - (count - 1) * buf_size;
+      // Averaging needs a previous full part to merge with.
+      const bool avg = last < min_part && count >= 2;
+      const uint64_t full = avg ? count - 1 : count;
+      for (uint64_t i = 1; i < full; ++i) add(i, (i - 1) * buf_size, buf_size);
+      if (!avg) {
+        add(count, (count - 1) * buf_size, last);
+      } else {
+        const uint64_t sz1 = (last + buf_size) / 2;
+        const uint64_t sz2 = last + buf_size - sz1;
+        add(full, (full - 1) * buf_size, sz1);
+        add(count, (full - 1) * buf_size + sz1, sz2);
+      }
+    }
+  } catch (...) {
+    return fail(-ENOMEM, "qsmd5: host allocation failed");
+  }
+  *nparts = v.size();
+  if (parts && cap) memcpy(parts, v.data(), std::min(cap, v.size()) * sizeof(qsmd5_part));
+  return cap && cap < v.size() ? fail(-EINVAL, "qsmd5: parts capacity too small") : 0;
+}
+
+int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t n, uint8_t (*digests)[16]) {
+  return guarded([&] {
+    if (n == 0) return 0;
+    if (!parts || !digests) return fail(-EINVAL, "qsmd5: NULL parts/digests");
+    std::vector<qsmd5_chunk> c(n);
+    const uint64_t base = parts[0].offset;
+    for (size_t i = 0; i < n; ++i) {
+      if (parts[i].offset < base) return fail(-EINVAL, "qsmd5: part offset before parts[0]");
+      c[i].ptr = static_cast<const uint8_t*>(file) + (parts[i].offset - base);
+      c[i].len = parts[i].size;
+    }
+    return qsmd5_hash_batch_ex(c.data(), n, digests, 0);
+  });
+}
+
+int qsmd5_last_timing(double* wall_ms, double* kernel_ms) {
+  Runtime& r = rt();
+  std::lock_guard<std::mutex> lk(r.mu);
+  if (wall_ms) *wall_ms = r.last_wall_ms;
+  if (kernel_ms) *kernel_ms = r.last_kernel_ms;
+  return 0;
+}
+
+int qsmd5_synth_fill_lcg(void* d_base, uint64_t stride, uint64_t len, uint32_t seed0,
+                         uint32_t nchunks, void* hip_stream) {
+  return guarded([&] {
+    if (!d_base && len && nchunks) return fail(-EINVAL, "qsmd5: NULL base");
+    if (int rc = ensure_init()) return rc;
+    hipError_t e = qsmd5::launch_lcg_fill(static_cast<uint8_t*>(d_base), stride, len, seed0,
+                                          nchunks, static_cast<hipStream_t>(hip_stream));
+    if (e != hipSuccess) return hip_fail(e, "qsmd5 fill launch");
+    return 0;
+  });
+}
+
+// ---- streaming context -------------------------------------------------------
+
+int qsmd5_ctx_create(qsmd5_ctx** out) {
+  return guarded([&] {
+    if (!out) return fail(-EINVAL, "qsmd5: NULL out");
+    *out = nullptr;
+    if (int rc = ensure_init()) return rc;
+    qsmd5_ctx* c = new qsmd5_ctx;
+    const uint32_t init[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    hipError_t e = hipMalloc(&c->d_state, 16);
+    if (e == hipSuccess) e = hipMalloc(&c->d_tail, 64);
+    if (e == hipSuccess) e = hipMemcpy(c->d_state, init, 16, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      qsmd5_ctx_destroy(c);
+      return hip_fail(e, "qsmd5_ctx_create");
+    }
+    *out = c;
+    return 0;
+  });
+}
+
+void qsmd5_ctx_destroy(qsmd5_ctx* c) {
+  if (!c) return;
+  if (c->d_state) (void)hipFree(c->d_state);
+  if (c->d_tail) (void)hipFree(c->d_tail);
+  if (c->d_stage) (void)hipFree(c->d_stage);
+  delete c;
+}
+
+static int ctx_blocks(qsmd5_ctx* c, const uint8_t* p, uint64_t nblk, bool on_device) {
+  Runtime& r = rt();
+  hipStream_t s = r.compute[0];
+  const uint8_t* src = p;
+  if (!on_device) {
+    const uint64_t bytes = nblk * 64;
+    if (bytes > c->stage_cap) {
+      if (c->d_stage) (void)hipFree(c->d_stage);
+      c->d_stage = nullptr;
+      c->stage_cap = 0;
+      QS_HIP(hipMalloc(&c->d_stage, bytes));
+      c->stage_cap = bytes;
+    }
+    QS_HIP(hipMemcpyAsync(c->d_stage, p, bytes, hipMemcpyHostToDevice, s));
+    src = c->d_stage;
+  }
+  while (nblk) {
+    const uint32_t step = (uint32_t)std::min<uint64_t>(nblk, 0x40000000ull);
+    QS_HIP(qsmd5::launch_blocks(c->d_state, src, step, s));
+    src += (uint64_t)step * 64;
+    nblk -= step;
+  }
+  QS_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+int qsmd5_ctx_update(qsmd5_ctx* c, const void* ptr, uint64_t len) {
+  return guarded([&] {
+    if (!c) return fail(-EINVAL, "qsmd5: NULL ctx");
+    if (c->finalized) return fail(-EINVAL, "qsmd5: update after final");
+    if (len == 0) return 0;
+    if (!ptr) return fail(-EINVAL, "qsmd5: NULL ptr with non-zero len");
+    if (int rc = ensure_init()) return rc;
+    std::lock_guard<std::mutex> lk(rt().mu);
+    const bool dev = classify(ptr) == kDeviceMem;
+    const uint8_t* p = static_cast<const uint8_t*>(ptr);
+    uint64_t left = len;
+    c->total += len;
+    if (c->tail_len) {
+      const uint32_t take = (uint32_t)std::min<uint64_t>(64 - c->tail_len, left);
+      if (dev) {
+        QS_HIP(hipMemcpy(c->tail + c->tail_len, p, take, hipMemcpyDeviceToHost));
+      } else {
+        memcpy(c->tail + c->tail_len, p, take);
+      }
+      c->tail_len += take;
+      p += take;
+      left -= take;
+      if (c->tail_len == 64) {
+        if (int rc = ctx_blocks(c, c->tail, 1, false)) return rc;
+        c->tail_len = 0;
+      }
+    }
+    const uint64_t nblk = left / 64;
+    if (nblk) {
+      if (int rc = ctx_blocks(c, p, nblk, dev)) return rc;
+      p += nblk * 64;
+      left -= nblk * 64;
+    }
+    if (left) {
+      if (dev) {
+        QS_HIP(hipMemcpy(c->tail, p, left, hipMemcpyDeviceToHost));
+      } else {
+        memcpy(c->tail, p, left);
+      }
+      c->tail_len = (uint32_t)left;
+    }
+    return 0;
+  });
+}
+
+int qsmd5_ctx_final(qsmd5_ctx* c, uint8_t digest[16]) {
+  return guarded([&] {
+    if (!c || !digest) return fail(-EINVAL, "qsmd5: NULL ctx/digest");
+    if (!c->finalized) {
+      if (int rc = ensure_init()) return rc;
+      std::lock_guard<std::mutex> lk(rt().mu);
+      hipStream_t s = rt().compute[0];
+      QS_HIP(hipMemcpyAsync(c->d_tail, c->tail, 64, hipMemcpyHostToDevice, s));
+      QS_HIP(qsmd5::launch_final(c->d_state, c->d_tail, c->tail_len, c->total, s));
+      QS_HIP(hipMemcpyAsync(c->digest, c->d_state, 16, hipMemcpyDeviceToHost, s));
+      QS_HIP(hipStreamSynchronize(s));
+      c->finalized = true;
+    }
+    memcpy(digest, c->digest, 16);
+    return 0;
+  });
+}
+
+}  // extern "C"

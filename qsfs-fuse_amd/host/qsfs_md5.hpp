@@ -1,0 +1,172 @@
+// qsfs-fuse_amd/host/qsfs_md5.hpp -- C++ drop-in for qsfs's src/base/MD5.h.
+//
+// Header-only layer over the C-ABI (include/qsmd5.h) that keeps the
+// reference's interface so QSClient compiles unchanged apart from the include:
+//
+//   std::string md5(const std::string)                 MD5.h:95, MD5.cpp:335-339
+//   std::string md5(const shared_ptr<std::iostream>&)  MD5.h:96, MD5.cpp:341-349
+//   class MD5 { update; finalize; hexdigest; << }      MD5.h:51-93
+//
+// md5(stream) hashes exactly the bytes the reference hashes -- from position 0
+// to the end of the stream's get area, i.e. the first lengthToRead bytes of a
+// qsfs StreamBuf (StreamBuf.cpp:32-48) -- and, like the reference, leaves the
+// read position at 0 (MD5.cpp:343, 346).  Unlike the reference it does not
+// copy the buffer twice through a stringstream (MD5.cpp:342-345): when the
+// stream buffer exposes its whole content as the get area (StreamBuf does),
+// the bytes are handed to the GPU in place.
+//
+// Failure: the reference could only throw std::bad_alloc.  A GPU failure here
+// throws qsmd5::Error (a std::runtime_error) -- a Content-MD5 must never
+// silently become "".
+//
+// The stream overload is a template over the smart-pointer type, so it accepts
+// boost::shared_ptr<std::iostream> (what qsfs passes) and std::shared_ptr alike.
+#ifndef QSFS_AMD_QSFS_MD5_HPP_
+#define QSFS_AMD_QSFS_MD5_HPP_
+
+#include <cstring>
+#include <iostream>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/qsmd5.h"
+
+namespace qsmd5 {
+
+class Error : public std::runtime_error {
+ public:
+  Error(int code, const char* what)
+      : std::runtime_error(std::string(what) + ": " + qsmd5_strerror(code) + " (" +
+                           qsmd5_last_error() + ")"),
+        code_(code) {}
+  int code() const { return code_; }
+
+ private:
+  int code_;
+};
+
+namespace detail {
+
+// Access to the protected get-area pointers of any std::streambuf.
+struct GetArea : std::streambuf {
+  using std::streambuf::eback;
+  using std::streambuf::egptr;
+  using std::streambuf::gptr;
+};
+
+inline std::string hex(const uint8_t d[16]) {
+  char b[33];
+  qsmd5_hex(d, b);
+  return std::string(b, 32);
+}
+
+inline void check(int rc, const char* what) {
+  if (rc != 0) throw Error(rc, what);
+}
+
+}  // namespace detail
+
+// MD5 of [p, p + len) as 32 lowercase hex characters.
+inline std::string md5_bytes(const void* p, uint64_t len) {
+  uint8_t d[16];
+  detail::check(qsmd5_hash_one(p, len, d), "qsmd5_hash_one");
+  return detail::hex(d);
+}
+
+// md5(const std::string) -- MD5.cpp:335-339.
+inline std::string md5(const std::string& str) { return md5_bytes(str.data(), str.size()); }
+
+namespace detail {
+// Enabled for anything with ->seekg / ->rdbuf (boost/std shared_ptr<iostream>).
+template <class P>
+using if_stream_ptr = decltype(std::declval<const P&>()->rdbuf(),
+                               std::declval<const P&>()->seekg(0, std::ios_base::beg), 0);
+}  // namespace detail
+
+// md5(const shared_ptr<iostream>&) -- MD5.cpp:341-349.
+template <class StreamPtr, detail::if_stream_ptr<StreamPtr> = 0>
+std::string md5(const StreamPtr& stream) {
+  stream->seekg(0, std::ios_base::beg);
+  std::streambuf* sb = stream->rdbuf();
+  std::string out;
+  if (sb) {
+    char* (std::streambuf::*p_gptr)() const = &detail::GetArea::gptr;
+    char* (std::streambuf::*p_egptr)() const = &detail::GetArea::egptr;
+    // Zero-copy only when the get area is the whole remaining content.
+    const std::streamoff end = sb->pubseekoff(0, std::ios_base::end, std::ios_base::in);
+    sb->pubseekoff(0, std::ios_base::beg, std::ios_base::in);
+    const char* g = (sb->*p_gptr)();
+    const char* e = (sb->*p_egptr)();
+    if (g && e >= g && end >= 0 && std::streamoff(e - g) == end) {
+      out = md5_bytes(g, static_cast<uint64_t>(e - g));
+    } else {
+      std::vector<char> buf;
+      char tmp[1 << 16];
+      std::streamsize got;
+      while ((got = sb->sgetn(tmp, sizeof tmp)) > 0) buf.insert(buf.end(), tmp, tmp + got);
+      out = md5_bytes(buf.data(), buf.size());
+    }
+  } else {
+    out = md5_bytes(nullptr, 0);
+  }
+  stream->clear();
+  stream->seekg(0, std::ios_base::beg);
+  return out;
+}
+
+// class MD5 -- MD5.h:51-93, over the streaming C-ABI context.
+class MD5 {
+ public:
+  typedef unsigned int size_type;  // as the reference (MD5.h:53)
+
+  MD5() { detail::check(qsmd5_ctx_create(&ctx_), "qsmd5_ctx_create"); }
+  explicit MD5(const std::string& text) : MD5() {
+    update(text.c_str(), static_cast<size_type>(text.length()));
+    finalize();
+  }
+  MD5(const MD5&) = delete;
+  MD5& operator=(const MD5&) = delete;
+  MD5(MD5&& o) noexcept : ctx_(o.ctx_), finalized_(o.finalized_) {
+    std::memcpy(digest_, o.digest_, 16);
+    o.ctx_ = nullptr;
+  }
+  ~MD5() { qsmd5_ctx_destroy(ctx_); }
+
+  void update(const unsigned char* buf, size_type length) {
+    detail::check(qsmd5_ctx_update(ctx_, buf, length), "qsmd5_ctx_update");
+  }
+  void update(const char* buf, size_type length) {
+    update(reinterpret_cast<const unsigned char*>(buf), length);
+  }
+  MD5& finalize() {
+    if (!finalized_) {
+      detail::check(qsmd5_ctx_final(ctx_, digest_), "qsmd5_ctx_final");
+      finalized_ = true;
+    }
+    return *this;
+  }
+  // "" until finalize(), as MD5.cpp:318.
+  std::string hexdigest() const { return finalized_ ? detail::hex(digest_) : std::string(); }
+  friend std::ostream& operator<<(std::ostream& os, const MD5& m) { return os << m.hexdigest(); }
+
+ private:
+  qsmd5_ctx* ctx_ = nullptr;
+  bool finalized_ = false;
+  uint8_t digest_[16] = {0};
+};
+
+}  // namespace qsmd5
+
+#ifndef QSMD5_NO_GLOBAL_MD5
+// The reference declares md5() at global scope (MD5.h:95-96); so does this
+// drop-in, unless QSMD5_NO_GLOBAL_MD5 is defined.
+inline std::string md5(const std::string& str) { return qsmd5::md5(str); }
+template <class StreamPtr, qsmd5::detail::if_stream_ptr<StreamPtr> = 0>
+inline std::string md5(const StreamPtr& stream) {
+  return qsmd5::md5(stream);
+}
+#endif
+
+#endif  // QSFS_AMD_QSFS_MD5_HPP_

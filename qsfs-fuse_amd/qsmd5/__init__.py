@@ -1,0 +1,314 @@
+"""qsmd5 -- Python binding of the MI355X MD5 chunk-hashing path (include/qsmd5.h).
+
+Thin ctypes layer over ``qsfs-fuse_amd/lib/libqsmd5.so``; tests, bench.py and
+__graft_entry__ use it.  It mirrors the reference interface names:
+
+  md5(data) -> str              std::string md5(const std::string)   MD5.cpp:335-339
+  md5_stream(stream) -> str     std::string md5(shared_ptr<iostream>) MD5.cpp:341-349
+  MD5().update(b).finalize().hexdigest()   class MD5                MD5.h:51-93
+
+plus the batch entry points the reference lacks (hash_batch, hash_parts,
+hash_device).  Hashing runs on the GPU only: if the library is missing this
+module raises on import-time use (``lib()``), and without a GPU every hashing
+call raises ``Md5Error`` with -ENODEV -- there is no CPU fallback.
+"""
+import ctypes
+import errno
+import os
+
+__all__ = [
+    "Md5Error", "lib", "lib_path", "hexdigest", "md5", "md5_stream", "MD5", "hash_batch",
+    "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
+    "alloc_pinned", "free_pinned", "synth_fill_lcg", "last_timing", "Part",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG_ROOT = os.path.dirname(_HERE)
+
+
+def lib_path():
+    return os.environ.get("QSMD5_LIB", os.path.join(_PKG_ROOT, "lib", "libqsmd5.so"))
+
+
+class Md5Error(RuntimeError):
+    def __init__(self, code, what):
+        self.code = code
+        super().__init__("%s failed: %d (%s)" % (what, code, _detail(code)))
+
+
+class qsmd5_chunk(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("len", ctypes.c_uint64)]
+
+
+class Part(ctypes.Structure):
+    """qsmd5_part: one multipart-upload part (QSTransferManager.cpp:475-550)."""
+    _fields_ = [("part_number", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("offset", ctypes.c_uint64), ("size", ctypes.c_uint64)]
+
+    def __repr__(self):
+        return "Part(%d, off=%d, size=%d)" % (self.part_number, self.offset, self.size)
+
+    def astuple(self):
+        return (self.part_number, self.offset, self.size)
+
+
+_lib = None
+
+
+def lib():
+    """Load libqsmd5.so (raises OSError loudly if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        raise OSError("libqsmd5.so not built at %s (run __graft_entry__.build())" % path)
+    L = ctypes.CDLL(path)
+    c_u8p = ctypes.POINTER(ctypes.c_uint8)
+    sig = {
+        "qsmd5_init": (ctypes.c_int, [ctypes.c_int]),
+        "qsmd5_abi_version": (ctypes.c_int, []),
+        "qsmd5_device_count": (ctypes.c_int, []),
+        "qsmd5_strerror": (ctypes.c_char_p, [ctypes.c_int]),
+        "qsmd5_last_error": (ctypes.c_char_p, []),
+        "qsmd5_hash_one": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, c_u8p]),
+        "qsmd5_hash_batch": (ctypes.c_int, [ctypes.POINTER(qsmd5_chunk), ctypes.c_size_t, c_u8p]),
+        "qsmd5_hash_batch_ex": (ctypes.c_int, [ctypes.POINTER(qsmd5_chunk), ctypes.c_size_t,
+                                               c_u8p, ctypes.c_int]),
+        "qsmd5_hash_batch_device_async": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p,
+                                                         ctypes.c_size_t, ctypes.c_void_p,
+                                                         ctypes.c_void_p]),
+        "qsmd5_kernel_choice": (ctypes.c_int, [ctypes.c_size_t]),
+        "qsmd5_hex": (None, [c_u8p, ctypes.c_char_p]),
+        "qsmd5_ctx_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
+        "qsmd5_ctx_update": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
+        "qsmd5_ctx_final": (ctypes.c_int, [ctypes.c_void_p, c_u8p]),
+        "qsmd5_ctx_destroy": (None, [ctypes.c_void_p]),
+        "qsmd5_alloc_pinned": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+        "qsmd5_free_pinned": (ctypes.c_int, [ctypes.c_void_p]),
+        "qsmd5_plan_parts": (ctypes.c_int, [ctypes.c_uint64] * 5 + [
+            ctypes.POINTER(Part), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
+        "qsmd5_hash_parts": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Part), ctypes.c_size_t,
+                                            c_u8p]),
+        "qsmd5_last_timing": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double),
+                                             ctypes.POINTER(ctypes.c_double)]),
+        "qsmd5_synth_fill_lcg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_uint32, ctypes.c_uint32,
+                                                ctypes.c_void_p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def _detail(code):
+    try:
+        L = lib()
+        return "%s; %s" % (L.qsmd5_strerror(code).decode(), L.qsmd5_last_error().decode())
+    except OSError:
+        return os.strerror(-code) if code < 0 else str(code)
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise Md5Error(rc, what)
+
+
+def device_count():
+    return lib().qsmd5_device_count()
+
+
+def kernel_choice(n):
+    return lib().qsmd5_kernel_choice(n)
+
+
+def hexdigest(digest):
+    """16 raw bytes -> 32 lowercase hex chars via qsmd5_hex (MD5.cpp:317-325)."""
+    d = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(digest))
+    out = ctypes.create_string_buffer(33)
+    lib().qsmd5_hex(d, out)
+    return out.value.decode()
+
+
+# ---- buffers -------------------------------------------------------------------------
+
+def _as_chunk(buf, keep):
+    """(ptr, len) of bytes/bytearray/memoryview/numpy/torch tensor (any device)."""
+    try:
+        import torch  # noqa: F401
+        if isinstance(buf, torch.Tensor):
+            if not buf.is_contiguous():
+                raise ValueError("tensor must be contiguous")
+            return buf.data_ptr(), buf.numel() * buf.element_size()
+    except ImportError:
+        pass
+    if isinstance(buf, tuple) and len(buf) == 2:  # raw (ptr, len)
+        return int(buf[0]), int(buf[1])
+    if isinstance(buf, bytes):
+        cb = ctypes.c_char_p(buf)
+        keep.append(cb)
+        return ctypes.cast(cb, ctypes.c_void_p).value, len(buf)
+    mv = memoryview(buf)
+    if not mv.contiguous:
+        raise ValueError("buffer must be contiguous")
+    n = mv.nbytes
+    if n == 0:
+        return 0, 0
+    if mv.readonly:
+        # read-only views (e.g. slices of bytes): borrow without copying
+        import numpy as np
+        a = np.frombuffer(mv, dtype=np.uint8)
+        keep.append(a)
+        return a.ctypes.data, n
+    c = (ctypes.c_uint8 * n).from_buffer(mv)
+    keep.append(c)
+    return ctypes.addressof(c), n
+
+
+def hash_batch(buffers, flags=0):
+    """MD5 of every buffer (host or device), one GPU batch -> list of 16-byte digests."""
+    bufs = list(buffers)
+    n = len(bufs)
+    if n == 0:
+        return []
+    keep = []
+    arr = (qsmd5_chunk * n)()
+    for i, b in enumerate(bufs):
+        p, L = _as_chunk(b, keep)
+        arr[i].ptr = p
+        arr[i].len = L
+    out = (ctypes.c_uint8 * (16 * n))()
+    _check(lib().qsmd5_hash_batch_ex(arr, n, out, flags), "qsmd5_hash_batch")
+    raw = bytes(out)
+    return [raw[16 * i:16 * i + 16] for i in range(n)]
+
+
+def hash_one(buf):
+    keep = []
+    p, L = _as_chunk(buf, keep)
+    out = (ctypes.c_uint8 * 16)()
+    _check(lib().qsmd5_hash_one(p, L, out), "qsmd5_hash_one")
+    return bytes(out)
+
+
+def md5(data):
+    """Mirror of the reference free function md5(std::string) -> lowercase hex."""
+    if isinstance(data, str):
+        data = data.encode("latin-1")
+    return hexdigest(hash_one(data))
+
+
+def md5_stream(stream):
+    """Mirror of md5(shared_ptr<iostream>) (MD5.cpp:341-349): hash the stream's
+    bytes from position 0 to its end and leave the read position at 0."""
+    stream.seek(0)
+    data = stream.read()
+    stream.seek(0)
+    if isinstance(data, str):
+        data = data.encode("latin-1")
+    return md5(data)
+
+
+def hash_device(chunks_dev, digests_dev, n, order_dev=None, stream=0):
+    """Enqueue qsmd5_hash_batch_device_async.  chunks_dev: device tensor holding n
+    qsmd5_chunk records (int64 pairs); digests_dev: device uint8 tensor [n,16]."""
+    _check(lib().qsmd5_hash_batch_device_async(
+        ctypes.c_void_p(int(chunks_dev)), ctypes.c_void_p(int(order_dev or 0)), n,
+        ctypes.c_void_p(int(digests_dev)), ctypes.c_void_p(int(stream or 0))),
+        "qsmd5_hash_batch_device_async")
+
+
+def plan_parts(file_size, buf_size=10 << 20, min_part=4 << 20, threshold=20 << 20,
+               range_begin=0):
+    """QSTransferManager::PrepareUpload slicing -> list of Part."""
+    L = lib()
+    need = ctypes.c_size_t(0)
+    _check(L.qsmd5_plan_parts(file_size, buf_size, min_part, threshold, range_begin, None, 0,
+                              ctypes.byref(need)), "qsmd5_plan_parts")
+    arr = (Part * max(need.value, 1))()
+    _check(L.qsmd5_plan_parts(file_size, buf_size, min_part, threshold, range_begin, arr,
+                              need.value, ctypes.byref(need)), "qsmd5_plan_parts")
+    return [arr[i] for i in range(need.value)]
+
+
+def hash_parts(file_buf, parts):
+    """Batch pre-hash of all parts of one file buffer (host or device)."""
+    keep = []
+    p, _ = _as_chunk(file_buf, keep)
+    n = len(parts)
+    if n == 0:
+        return []
+    arr = (Part * n)(*parts)
+    out = (ctypes.c_uint8 * (16 * n))()
+    _check(lib().qsmd5_hash_parts(p, arr, n, out), "qsmd5_hash_parts")
+    raw = bytes(out)
+    return [raw[16 * i:16 * i + 16] for i in range(n)]
+
+
+class MD5(object):
+    """Mirror of the reference class MD5 (MD5.h:51-93) over qsmd5_ctx."""
+
+    def __init__(self, text=None):
+        self._ctx = ctypes.c_void_p()
+        _check(lib().qsmd5_ctx_create(ctypes.byref(self._ctx)), "qsmd5_ctx_create")
+        self._digest = None
+        if text is not None:
+            self.update(text)
+            self.finalize()
+
+    def update(self, data):
+        if isinstance(data, str):
+            data = data.encode("latin-1")
+        keep = []
+        p, L = _as_chunk(data, keep)
+        _check(lib().qsmd5_ctx_update(self._ctx, p, L), "qsmd5_ctx_update")
+        return self
+
+    def finalize(self):
+        if self._digest is None:
+            out = (ctypes.c_uint8 * 16)()
+            _check(lib().qsmd5_ctx_final(self._ctx, out), "qsmd5_ctx_final")
+            self._digest = bytes(out)
+        return self
+
+    def digest(self):
+        return self._digest
+
+    def hexdigest(self):
+        # MD5::hexdigest returns "" before finalize (MD5.cpp:318)
+        return hexdigest(self._digest) if self._digest is not None else ""
+
+    def __del__(self):
+        try:
+            if self._ctx:
+                lib().qsmd5_ctx_destroy(self._ctx)
+                self._ctx = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+def alloc_pinned(nbytes):
+    p = ctypes.c_void_p()
+    _check(lib().qsmd5_alloc_pinned(nbytes, ctypes.byref(p)), "qsmd5_alloc_pinned")
+    return p.value
+
+
+def free_pinned(ptr):
+    _check(lib().qsmd5_free_pinned(ctypes.c_void_p(ptr)), "qsmd5_free_pinned")
+
+
+def synth_fill_lcg(base_ptr, stride, length, seed0, nchunks, stream=0):
+    _check(lib().qsmd5_synth_fill_lcg(ctypes.c_void_p(base_ptr), stride, length, seed0, nchunks,
+                                      ctypes.c_void_p(int(stream or 0))), "qsmd5_synth_fill_lcg")
+
+
+def last_timing():
+    w, k = ctypes.c_double(), ctypes.c_double()
+    lib().qsmd5_last_timing(ctypes.byref(w), ctypes.byref(k))
+    return w.value, k.value
+
+
+ENODEV = -errno.ENODEV

@@ -1,0 +1,49 @@
+"""pytest configuration: the `gpu` marker, import paths, shared fixtures.
+
+`-m "not gpu"` tests run on any CPU box: the oracle against the golden
+fixtures, host-only C-ABI logic (hex, part planning), the exported-symbol
+check of libqsmd5.so, and the multi-rank digest gather over gloo.
+`-m gpu` tests are the parity tests proper: every digest through the C-ABI on
+an MI355X against the committed golden fixtures (produced by the reference's
+own MD5.cpp) and the oracle.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "qsfs-fuse_amd"), os.path.join(ROOT, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+
+
+def _ensure_built():
+    """Build oracle/ and libqsmd5.so in place if a fresh checkout lacks them."""
+    oracle_so = os.path.join(ROOT, "oracle", "libmd5_oracle.so")
+    lib_so = os.path.join(ROOT, "qsfs-fuse_amd", "lib", "libqsmd5.so")
+    if not os.path.exists(oracle_so):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "libmd5_oracle.so"])
+    if not os.path.exists(lib_so):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "qsfs-fuse_amd"), "-j4"])
+
+
+_ensure_built()
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden():
+    return load_golden

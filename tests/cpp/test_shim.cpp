@@ -1,0 +1,137 @@
+// tests/cpp/test_shim.cpp -- drop-in checks for qsfs-fuse_amd/host/qsfs_md5.hpp.
+//
+// Exercises the reference-shaped C++ interface on the GPU and prints one
+// "name hexdigest" line per case; tests/test_gpu_shim.py compares every line
+// with hashlib.  Also asserts the stream side effects of the reference
+// md5(shared_ptr<iostream>) (MD5.cpp:343, 346: read position reset to 0) and
+// the StreamBuf view contract (StreamBuf.cpp:32-48; StreamTest.cpp:131-150:
+// a stream over a 3-byte buffer with lengthToRead=2 exposes "01").
+#include <cstdio>
+#include <cstdlib>
+#include <memory>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../qsfs-fuse_amd/host/qsfs_md5.hpp"
+
+namespace {
+
+// The qsfs StreamBuf contract: a view of the first `len` bytes of a shared
+// vector<char> (StreamBuf.cpp:32-48), seekable (StreamBuf.cpp:56-91).
+class ViewBuf : public std::streambuf {
+ public:
+  ViewBuf(std::shared_ptr<std::vector<char>> buf, size_t len) : buf_(std::move(buf)), len_(len) {
+    char* b = buf_->data();
+    setp(b, b + len_);
+    setg(b, b, b + len_);
+  }
+
+ protected:
+  pos_type seekoff(off_type off, std::ios_base::seekdir dir, std::ios_base::openmode which) override {
+    if (dir == std::ios_base::beg) return seekpos(off, which);
+    if (dir == std::ios_base::end) return seekpos(off_type(len_) - off, which);
+    return seekpos((gptr() - eback()) + off, which);
+  }
+  pos_type seekpos(pos_type pos, std::ios_base::openmode) override {
+    if (pos < 0 || pos > off_type(len_)) return pos_type(off_type(-1));
+    char* b = buf_->data();
+    setg(b, b + off_type(pos), b + len_);
+    return pos;
+  }
+
+ private:
+  std::shared_ptr<std::vector<char>> buf_;
+  size_t len_;
+};
+
+class ViewStream : public std::iostream {
+ public:
+  ViewStream(std::shared_ptr<std::vector<char>> buf, size_t len) : std::iostream(nullptr), sb_(buf, len) {
+    rdbuf(&sb_);
+  }
+
+ private:
+  ViewBuf sb_;
+};
+
+std::vector<char> lcg(uint32_t seed, size_t n) {
+  std::vector<char> v(n);
+  uint32_t x = seed;
+  for (size_t i = 0; i < n; ++i) {
+    x = x * 1103515245u + 12345u;
+    v[i] = static_cast<char>(x >> 16);
+  }
+  return v;
+}
+
+int failures = 0;
+void expect(bool ok, const char* what) {
+  if (!ok) {
+    std::fprintf(stderr, "FAIL: %s\n", what);
+    ++failures;
+  }
+}
+
+}  // namespace
+
+int main() {
+  // 1. md5(std::string) -- global, as the reference's free function.
+  std::printf("str_empty %s\n", md5(std::string()).c_str());
+  std::printf("str_abc %s\n", md5(std::string("abc")).c_str());
+  std::printf("str_literal %s\n", md5("message digest").c_str());
+
+  // 2. md5(shared_ptr<iostream>) over a StreamBuf-style view (lengthToRead < size).
+  for (size_t len : {size_t(0), size_t(2), size_t(55), size_t(64), size_t(10485760)}) {
+    auto buf = std::make_shared<std::vector<char>>(lcg(12345, len + 100));
+    std::shared_ptr<std::iostream> s = std::make_shared<ViewStream>(buf, len);
+    s->seekg(7, std::ios_base::beg);  // position before the call must not matter
+    std::string h = md5(s);
+    std::printf("view_%zu %s\n", len, h.c_str());
+    expect(s->tellg() == std::streampos(0), "read position reset to 0 after md5(stream)");
+    expect(md5(s) == h, "md5(stream) is repeatable");
+  }
+  // StreamTest Read1: 3-byte buffer, lengthToRead = 2 -> hashes "01".
+  {
+    auto buf = std::make_shared<std::vector<char>>(std::vector<char>{'0', '1', '2'});
+    std::shared_ptr<std::iostream> s = std::make_shared<ViewStream>(buf, 2);
+    std::printf("streamtest_read1 %s\n", md5(s).c_str());
+  }
+  // 3. A stream whose get area is not the whole content (stringstream):
+  //    falls back to reading through the streambuf.
+  {
+    std::shared_ptr<std::iostream> s = std::make_shared<std::stringstream>();
+    std::string payload(100000, 'q');
+    *s << payload;
+    std::printf("stringstream_100000q %s\n", md5(s).c_str());
+  }
+  // 4. class MD5: update in pieces, finalize, hexdigest, operator<<.
+  {
+    std::vector<char> d = lcg(4242, 200000);
+    qsmd5::MD5 m;
+    expect(m.hexdigest().empty(), "hexdigest empty before finalize");
+    size_t off = 0;
+    for (unsigned cut : {63u, 1u, 64u, 65u, 199807u}) {
+      m.update(d.data() + off, cut);
+      off += cut;
+    }
+    m.finalize();
+    std::ostringstream os;
+    os << m;
+    std::printf("class_pieces %s\n", os.str().c_str());
+    qsmd5::MD5 one(std::string("abc"));
+    std::printf("class_ctor_abc %s\n", one.hexdigest().c_str());
+  }
+  // 5. Errors are loud: NULL pointer with a non-zero length.
+  {
+    bool threw = false;
+    try {
+      qsmd5::md5_bytes(nullptr, 5);
+    } catch (const qsmd5::Error& e) {
+      threw = e.code() < 0;
+    }
+    expect(threw, "md5_bytes(NULL, 5) throws qsmd5::Error");
+  }
+  std::printf("failures %d\n", failures);
+  return failures ? 1 : 0;
+}

@@ -1,0 +1,147 @@
+"""Host-side checks of the C-ABI library (no GPU needed).
+
+- libqsmd5.so loads and exports every function include/qsmd5.h declares;
+- qsmd5_hex reproduces MD5::hexdigest (MD5.cpp:317-325);
+- qsmd5_plan_parts reproduces QSTransferManager::PrepareUpload slicing
+  (QSTransferManager.cpp:475-550), checked against the worked examples in
+  SURVEY.md §8(a) and a direct restatement of the reference's arithmetic;
+- without a GPU every hashing entry point fails loudly with -ENODEV (no CPU
+  fallback exists in the product path).
+"""
+import ctypes
+import errno
+import os
+import random
+import re
+import subprocess
+
+import pytest
+
+import qsmd5
+from conftest import ROOT
+
+MiB = 1 << 20
+GiB = 1 << 30
+
+
+def declared_functions():
+    text = open(os.path.join(ROOT, "include", "qsmd5.h")).read()
+    return sorted(set(re.findall(r"QSMD5_API\s+[\w\s\*]+?\b(qsmd5_\w+)\s*\(", text)))
+
+
+def test_header_declares_expected_surface():
+    names = declared_functions()
+    for must in ["qsmd5_init", "qsmd5_hash_one", "qsmd5_hash_batch", "qsmd5_hash_batch_device_async",
+                 "qsmd5_hex", "qsmd5_ctx_create", "qsmd5_ctx_update", "qsmd5_ctx_final",
+                 "qsmd5_ctx_destroy", "qsmd5_alloc_pinned", "qsmd5_free_pinned",
+                 "qsmd5_plan_parts", "qsmd5_hash_parts"]:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    so = qsmd5.lib_path()
+    L = ctypes.CDLL(so)
+    for name in declared_functions():
+        assert hasattr(L, name), name
+    out = subprocess.check_output(["nm", "-D", "--defined-only", so]).decode()
+    exported = set(re.findall(r" T (\w+)", out))
+    assert set(declared_functions()) == {s for s in exported if s.startswith("qsmd5_")}
+    # nothing but the C-ABI leaks (kernel stubs and launchers stay hidden)
+    assert not [s for s in exported if "device_stub" in s or "launch_" in s]
+
+
+def test_abi_version():
+    assert qsmd5.lib().qsmd5_abi_version() == 1
+
+
+def test_hex_matches_reference_format():
+    rng = random.Random(3)
+    for _ in range(100):
+        d = bytes(rng.getrandbits(8) for _ in range(16))
+        assert qsmd5.hexdigest(d) == "".join("%02x" % b for b in d)
+    assert qsmd5.hexdigest(b"\x00" * 16) == "0" * 32
+    assert qsmd5.hexdigest(b"\xff" * 16) == "f" * 32
+
+
+def prepare_upload_restated(total, buf, min_part, threshold):
+    """Direct restatement of QSTransferManager::PrepareUpload (QSTransferManager.cpp:492-546)."""
+    if total < threshold:
+        return [(1, 0, total)]
+    part_count = -(-total // buf)  # ceil(total / buf), exact for integers
+    last = total - (part_count - 1) * buf
+    avg = last < min_part
+    count = part_count - 1 if avg else part_count
+    parts = [(i, (i - 1) * buf, buf) for i in range(1, count)]
+    if not avg:
+        parts.append((part_count, (part_count - 1) * buf, last))
+    else:
+        sz1 = (last + buf) // 2
+        sz2 = last + buf - sz1
+        parts.append((count, (count - 1) * buf, sz1))
+        parts.append((part_count, (count - 1) * buf + sz1, sz2))
+    return parts
+
+
+def plan(total, **kw):
+    return [p.astuple() for p in qsmd5.plan_parts(total, **kw)]
+
+
+def test_plan_parts_survey_examples():
+    # 25 MiB -> [10,10,5]; 21 MiB -> [10, 5.5, 5.5]; 100 GiB -> 10240 x 10 MiB
+    assert [s for _, _, s in plan(25 * MiB)] == [10 * MiB, 10 * MiB, 5 * MiB]
+    p21 = plan(21 * MiB)
+    assert [s for _, _, s in p21] == [10 * MiB, 11 * MiB // 2, 11 * MiB // 2]
+    assert [n for n, _, _ in p21] == [1, 2, 3]
+    p100 = plan(100 * GiB)
+    assert len(p100) == 10240 and all(s == 10 * MiB for _, _, s in p100)
+    assert plan(19 * MiB) == [(1, 0, 19 * MiB)]  # below the 20 MiB threshold: PutObject
+    assert plan(0) == [(1, 0, 0)]
+    # odd remainder: the averaged pair must not lose the last byte
+    p = plan(20 * MiB + 3)
+    assert sum(s for _, _, s in p) == 20 * MiB + 3
+
+
+def test_plan_parts_matches_restatement_random():
+    rng = random.Random(11)
+    for _ in range(400):
+        buf = rng.choice([1, 2, 4, 8, 10, 16, 32, 64]) * MiB
+        total = rng.choice([rng.randrange(0, 200 * MiB), rng.randrange(0, 8 * GiB),
+                            20 * MiB + rng.randrange(-3, 4)])
+        want = prepare_upload_restated(total, buf, 4 * MiB, 20 * MiB)
+        got = plan(total, buf_size=buf)
+        if want and want[0][0] == 0:  # degenerate averaging with a single part
+            continue
+        assert got == want, (total, buf)
+        assert sum(s for _, _, s in got) == total
+        off = 0
+        for _, o, s in got:
+            assert o == off
+            off += s
+
+
+def test_plan_parts_range_begin_and_capacity():
+    p = plan(25 * MiB, range_begin=1000)
+    assert [o for _, o, _ in p] == [1000, 1000 + 10 * MiB, 1000 + 20 * MiB]
+    L = qsmd5.lib()
+    need = ctypes.c_size_t()
+    arr = (qsmd5.Part * 1)()
+    rc = L.qsmd5_plan_parts(25 * MiB, 10 * MiB, 4 * MiB, 20 * MiB, 0, arr, 1, ctypes.byref(need))
+    assert rc == -errno.EINVAL and need.value == 3
+    assert L.qsmd5_plan_parts(5, 0, 0, 0, 0, None, 0, ctypes.byref(need)) == -errno.EINVAL
+
+
+def test_strerror():
+    L = qsmd5.lib()
+    assert L.qsmd5_strerror(0) == b"success"
+    assert L.qsmd5_strerror(-errno.ENODEV) == b"no usable GPU"
+
+
+@pytest.mark.skipif(qsmd5.device_count() > 0, reason="GPU present")
+def test_no_gpu_fails_loudly():
+    with pytest.raises(qsmd5.Md5Error) as e:
+        qsmd5.hash_one(b"abc")
+    assert e.value.code == -errno.ENODEV
+    with pytest.raises(qsmd5.Md5Error):
+        qsmd5.hash_batch([b"abc", b"def"])
+    with pytest.raises(qsmd5.Md5Error):
+        qsmd5.MD5("abc")

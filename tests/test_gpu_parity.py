@@ -1,0 +1,272 @@
+"""Parity of the HIP path (through the C-ABI, libqsmd5.so) on an MI355X.
+
+Every digest is compared bit-exactly with the golden fixtures produced by the
+reference's own MD5.cpp (tests/golden/) or, for inputs the fixtures do not
+hold, with the CPU oracle on the same bytes.  Covers both kernels, host
+(pageable and pinned) and device memory, unaligned pointers, every padding
+edge, ragged batches, the streaming MD5 class, the part planner + batch
+pre-hash, >= 4 GiB lengths, concurrency and error behaviour.
+"""
+import ctypes
+import errno
+import os
+import threading
+
+import pytest
+
+import qsmd5
+from oracle_util import lcg_bytes, md5_many, md5_ref
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert qsmd5.lib().qsmd5_init(0) == 0
+    yield
+    os.environ.pop("QSMD5_KERNEL", None)
+
+
+@pytest.fixture(params=["pc", "v1"])
+def kernel(request):
+    os.environ["QSMD5_KERNEL"] = request.param
+    yield request.param
+    os.environ.pop("QSMD5_KERNEL", None)
+
+
+def dev_lcg(seed, n, nchunks=1, stride=None):
+    """Device tensor filled by the GPU LCG generator (qsmd5_synth_fill_lcg)."""
+    stride = stride or n
+    t = torch.empty(max(stride * nchunks, 1), dtype=torch.uint8, device="cuda")
+    qsmd5.synth_fill_lcg(t.data_ptr(), stride, n, seed, nchunks,
+                         torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return t
+
+
+def hexes(ds):
+    return [d.hex() for d in ds]
+
+
+def test_rfc1321(golden):
+    for c in golden("rfc1321.json")["cases"]:
+        assert qsmd5.md5(c["text"]) == c["md5"]
+
+
+def test_lcg_lengths_host(golden, kernel):
+    g = golden("lcg_lengths.json")
+    big = max(c["len"] for c in g["cases"])
+    data = lcg_bytes(12345, big)
+    base = ctypes.addressof(data)
+    got = qsmd5.hash_batch([(base, c["len"]) for c in g["cases"]])
+    assert hexes(got) == [c["md5"] for c in g["cases"]]
+
+
+def test_lcg_lengths_device(golden, kernel):
+    g = golden("lcg_lengths.json")
+    big = max(c["len"] for c in g["cases"])
+    t = dev_lcg(12345, big)
+    assert bytes(t[:64].cpu().numpy()) == bytes(lcg_bytes(12345, 64))  # generator parity
+    got = qsmd5.hash_batch([(t.data_ptr(), c["len"]) for c in g["cases"]])
+    assert hexes(got) == [c["md5"] for c in g["cases"]]
+
+
+def test_generator_matches_oracle():
+    for seed, n in [(1, 1), (2, 1023), (3, 1025), (12345, 3 * MiB + 7)]:
+        t = dev_lcg(seed, n)
+        assert bytes(t[:n].cpu().numpy()) == bytes(lcg_bytes(seed, n))[:n]
+
+
+def test_unaligned_device_pointers(kernel):
+    n = 1 << 20
+    t = dev_lcg(777, n)
+    host = bytes(t.cpu().numpy())
+    lens = [0, 1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 129, 4096, 8191, 65537, 300001]
+    chunks, want = [], []
+    for off in range(8):
+        for L in lens:
+            o = off * 4099 + off
+            chunks.append((t.data_ptr() + o, L))
+            want.append(md5_ref(host[o:o + L]))
+    assert qsmd5.hash_batch(chunks) == want
+
+
+def test_unaligned_host_pointers(kernel):
+    data = lcg_bytes(4321, 1 << 20)
+    base = ctypes.addressof(data)
+    raw = bytes(data)
+    chunks, want = [], []
+    for off in range(1, 8):
+        for L in [0, 1, 63, 64, 65, 1000, 100003]:
+            chunks.append((base + off, L))
+            want.append(md5_ref(raw[off:off + L]))
+    assert qsmd5.hash_batch(chunks) == want
+
+
+def test_ragged_batch_device(golden):
+    g = golden("ragged.json")
+    lens = g["lengths"]
+    offs, pos = [], 0
+    for L in lens:
+        offs.append(pos)
+        pos += (L + 255) & ~255
+    t = torch.empty(pos + 256, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        qsmd5.synth_fill_lcg(t.data_ptr() + o, 0, L, 7000 + i, 1, s)
+    torch.cuda.synchronize()
+    got = qsmd5.hash_batch([(t.data_ptr() + o, L) for o, L in zip(offs, lens)])
+    assert hexes(got) == g["md5"]
+
+
+def test_bufsize_sweep_device(golden):
+    for sw in golden("ragged.json")["sweep"]:
+        L = sw["mib"] * MiB
+        n = len(sw["md5"])
+        t = dev_lcg(sw["seed0"], L, nchunks=n)
+        got = qsmd5.hash_batch([(t.data_ptr() + i * L, L) for i in range(n)])
+        assert hexes(got) == sw["md5"], sw["mib"]
+
+
+def _device_batch(n, L, seed0):
+    t = dev_lcg(seed0, L, nchunks=n)
+    desc = torch.empty((n, 2), dtype=torch.int64)
+    desc[:, 0] = t.data_ptr() + torch.arange(n, dtype=torch.int64) * L
+    desc[:, 1] = L
+    return t, desc.cuda()
+
+
+def test_batch512_device_resident_async(golden):
+    """BASELINE config 2: 512 x 10 MiB device-resident, all 512 digests."""
+    g = golden("batch_10MiB.json")
+    n, L = 512, g["len"]
+    t, desc = _device_batch(n, L, 12345)
+    dig = torch.zeros((n, 16), dtype=torch.uint8, device="cuda")
+    qsmd5.hash_device(desc.data_ptr(), dig.data_ptr(), n,
+                      stream=torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = [bytes(r) for r in dig.cpu().numpy()]
+    assert hexes(got) == g["md5"][:n]
+
+
+def test_batch4096_device_resident(golden):
+    """Config 3 shape (4096 x 10 MiB) device-resident: every digest vs the fixture."""
+    g = golden("batch_10MiB.json")
+    n, L = 4096, g["len"]
+    t, desc = _device_batch(n, L, 12345)
+    got = qsmd5.hash_batch([(t.data_ptr() + i * L, L) for i in range(n)])
+    assert hexes(got) == g["md5"][:n]
+    del t
+
+
+def test_batch_pinned_host(golden):
+    g = golden("batch_10MiB.json")
+    n, L = 96, g["len"]
+    p = qsmd5.alloc_pinned(n * L)
+    try:
+        t = dev_lcg(12345, L, nchunks=n)
+        ctypes.memmove(p, bytes(t.cpu().numpy()), n * L)
+        del t
+        got = qsmd5.hash_batch([(p + i * L, L) for i in range(n)])
+        assert hexes(got) == g["md5"][:n]
+    finally:
+        qsmd5.free_pinned(p)
+
+
+def test_stream_pieces_class(golden):
+    g = golden("stream_pieces.json")
+    raw = bytes(lcg_bytes(g["seed"], g["len"]))
+    dev = torch.frombuffer(bytearray(raw), dtype=torch.uint8).cuda()
+    for case in g["cases"]:
+        m = qsmd5.MD5()
+        assert m.hexdigest() == ""
+        off = 0
+        for cut in case["cuts"]:
+            m.update(raw[off:off + cut])
+            off += cut
+        assert m.finalize().hexdigest() == case["md5"]
+        # the same pieces from device memory
+        m2 = qsmd5.MD5()
+        off = 0
+        for cut in case["cuts"]:
+            m2.update(dev[off:off + cut])
+            off += cut
+        assert m2.finalize().hexdigest() == case["md5"]
+    assert qsmd5.MD5("abc").hexdigest() == "900150983cd24fb0d6963f7d28e17f72"
+
+
+def test_md5_stream_mirror():
+    import io
+    s = io.BytesIO(b"0123456789" * 1000)
+    s.seek(17)
+    h = qsmd5.md5_stream(s)
+    assert h == md5_ref(b"0123456789" * 1000).hex() and s.tell() == 0
+
+
+def test_plan_and_hash_parts_host_and_device():
+    size = 100 * MiB + 12345  # 10 full parts + averaged pair
+    data = lcg_bytes(31337, size)
+    parts = qsmd5.plan_parts(size)
+    assert len(parts) == 11
+    raw = memoryview(data)
+    want = md5_many([(ctypes.addressof(data) + p.offset, p.size) for p in parts])
+    assert qsmd5.hash_parts(data, parts) == want
+    dev = dev_lcg(31337, size)
+    assert qsmd5.hash_parts(dev, parts) == want
+    del raw
+
+
+def test_length_over_4gib_truncation_flag(golden):
+    """>= 4 GiB: full RFC 1321 by default; the reference's 32-bit truncation on request."""
+    g = golden("truncate32.json")
+    L = g["len"]
+    t = dev_lcg(g["seed"], L)
+    full = qsmd5.hash_batch([(t.data_ptr(), L)])[0]
+    trunc = qsmd5.hash_batch([(t.data_ptr(), L)], flags=1)[0]
+    assert full.hex() == g["full_md5"]
+    assert trunc.hex() == g["reference_md5"]
+    del t
+
+
+def test_concurrent_callers():
+    data = [lcg_bytes(900 + i, 3 * MiB + i) for i in range(8)]
+    want = [md5_ref(d) for d in data]
+    errs = []
+
+    def worker(k):
+        try:
+            for _ in range(3):
+                got = qsmd5.hash_batch(data[k:] + data[:k])
+                assert got == want[k:] + want[:k]
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+
+
+def test_errors_and_empty():
+    L = qsmd5.lib()
+    out = (ctypes.c_uint8 * 16)()
+    assert L.qsmd5_hash_one(None, 5, out) == -errno.EINVAL
+    assert L.qsmd5_hash_one(ctypes.c_void_p(1), 1 << 38, out) == -errno.EINVAL
+    assert L.qsmd5_hash_one(None, 0, out) == 0
+    assert bytes(out).hex() == "d41d8cd98f00b204e9800998ecf8427e"
+    assert qsmd5.hash_batch([]) == []
+    assert L.qsmd5_hash_batch(None, 0, None) == 0
+
+
+def test_kernel_choice_policy():
+    os.environ.pop("QSMD5_KERNEL", None)
+    assert qsmd5.kernel_choice(512) == 1
+    assert qsmd5.kernel_choice(16384) == 1
+    assert qsmd5.kernel_choice(16385) == 0

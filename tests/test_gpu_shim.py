@@ -1,0 +1,49 @@
+"""The C++ drop-in (qsfs-fuse_amd/host/qsfs_md5.hpp) on the GPU.
+
+tests/cpp/test_shim.cpp uses the reference-shaped interface -- global
+md5(std::string), md5(shared_ptr<iostream>) over a qsfs StreamBuf-style view,
+class MD5 -- and prints one digest per case; each is checked here against
+hashlib / the oracle.  The binary also asserts the reference's stream side
+effects (read position reset to 0, MD5.cpp:343-346) and loud failure.
+"""
+import hashlib
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+from oracle_util import lcg_bytes
+
+pytestmark = pytest.mark.gpu
+
+BIN = os.path.join(ROOT, "tests", "cpp", "test_shim")
+
+
+def build_shim():
+    subprocess.check_call([
+        "g++", "-std=c++17", "-O2", os.path.join(ROOT, "tests", "cpp", "test_shim.cpp"),
+        "-I" + os.path.join(ROOT, "include"), "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"),
+        "-lqsmd5", "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-o", BIN])
+
+
+def test_cpp_dropin_shim():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if not os.path.exists(BIN):
+        build_shim()
+    out = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    got = dict(line.split() for line in out.stdout.strip().splitlines())
+    h = lambda b: hashlib.md5(b).hexdigest()
+    assert got["str_empty"] == h(b"")
+    assert got["str_abc"] == h(b"abc")
+    assert got["str_literal"] == h(b"message digest")
+    for L in (0, 2, 55, 64, 10485760):
+        assert got["view_%d" % L] == h(bytes(lcg_bytes(12345, L + 100))[:L]), L
+    assert got["streamtest_read1"] == h(b"01")
+    assert got["stringstream_100000q"] == h(b"q" * 100000)
+    assert got["class_pieces"] == h(bytes(lcg_bytes(4242, 200000)))
+    assert got["class_ctor_abc"] == h(b"abc")
+    assert got["failures"] == "0"

@@ -1,0 +1,317 @@
+// ubench/ubench_md5.hip -- gfx950 micro-measurements behind the MD5 kernel design.
+//
+// 1. VALU issue/latency for one wave alone on its SIMD (inline-asm loops timed
+//    with s_memtime): dependent vs independent v_add_u32, v_alignbit_b32,
+//    v_bitop3_b32, v_add3_u32.  These set the per-chain MD5 rate.
+// 2. qsmd5_batch_kernel on B chunks x L bytes of device-resident LCG data:
+//    wall time per launch (hipEvents) -> per-chain rate r1 and B*r1, with every
+//    digest checked against the CPU oracle.
+// Test infrastructure, not product code.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <vector>
+
+#include "../qsfs-fuse_amd/csrc/md5_kernels.hip"
+extern "C" {
+#include "../oracle/md5_oracle.c"
+}
+
+#define CK(x)                                                                      \
+  do {                                                                             \
+    hipError_t e_ = (x);                                                           \
+    if (e_ != hipSuccess) {                                                        \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, \
+              __LINE__);                                                           \
+      exit(2);                                                                     \
+    }                                                                              \
+  } while (0)
+
+// ---- 1. issue / latency ----------------------------------------------------
+#define REP8(x) x x x x x x x x
+#define REP64(x) REP8(REP8(x))
+
+__global__ void k_dep_add(uint64_t* out, uint32_t* sink, int iters) {
+  uint32_t v0 = threadIdx.x, v1 = 3;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    asm volatile(REP64("v_add_u32 %0, %0, %1\n") : "+v"(v0) : "v"(v1));
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = v0;
+}
+
+__global__ void k_ind_add(uint64_t* out, uint32_t* sink, int iters) {
+  uint32_t a = threadIdx.x, b = a + 1, c = a + 2, d = a + 3, one = 1;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    asm volatile(REP8(REP8("v_add_u32 %0, %0, %4\nv_add_u32 %1, %1, %4\nv_add_u32 %2, %2, %4\nv_add_u32 %3, %3, %4\n"))
+                 : "+v"(a), "+v"(b), "+v"(c), "+v"(d)
+                 : "v"(one));
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = a + b + c + d;
+}
+
+__global__ void k_dep_alignbit(uint64_t* out, uint32_t* sink, int iters) {
+  uint32_t v0 = threadIdx.x;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    asm volatile(REP64("v_alignbit_b32 %0, %0, %0, 7\n") : "+v"(v0));
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = v0;
+}
+
+__global__ void k_dep_bitop3(uint64_t* out, uint32_t* sink, int iters) {
+  uint32_t v0 = threadIdx.x, v1 = 5, v2 = 9;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    asm volatile(REP64("v_bitop3_b32 %0, %0, %1, %2 bitop3:0xca\n") : "+v"(v0) : "v"(v1), "v"(v2));
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = v0;
+}
+
+__global__ void k_dep_add3(uint64_t* out, uint32_t* sink, int iters) {
+  uint32_t v0 = threadIdx.x, v1 = 5, v2 = 9;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    asm volatile(REP64("v_add3_u32 %0, %0, %1, %2\n") : "+v"(v0) : "v"(v1), "v"(v2));
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = v0;
+}
+
+// MD5-shaped dependent step: bitop3 -> add3 -> alignbit -> add (4-deep chain)
+// plus one off-path add: 5 instructions / step.
+__global__ void k_md5_step(uint64_t* out, uint32_t* sink, int iters) {
+  uint32_t a = threadIdx.x, b = 1, c = 2, d = 3, m = 7, t = 0, s;
+  asm volatile("s_mov_b32 %0, 0x12345" : "=s"(s));
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    asm volatile(REP8(REP8(
+        "v_add3_u32 %4, %0, %5, %6\n"
+        "v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca\n"
+        "v_add_u32 %0, %0, %4\n"
+        "v_alignbit_b32 %0, %0, %0, 25\n"
+        "v_add_u32 %0, %0, %1\n"))
+                 : "+v"(a), "+v"(b), "+v"(c), "+v"(d), "+v"(t)
+                 : "v"(m), "s"(s));
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = a + b + c + d;
+}
+
+// MD5-shaped step with the a+x+k term precomputed elsewhere (4 instr/step).
+__global__ void k_md5_step4(uint64_t* out, uint32_t* sink, int iters) {
+  uint32_t a = threadIdx.x, b = 1, c = 2, d = 3, mk = 7;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    asm volatile(REP8(REP8(
+        "v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca\n"
+        "v_add3_u32 %0, %0, %4, %1\n"
+        "v_alignbit_b32 %0, %0, %0, 25\n"
+        "v_add_u32 %0, %0, %1\n"))
+                 : "+v"(a), "+v"(b), "+v"(c), "+v"(d)
+                 : "v"(mk));
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = a + b + c + d;
+}
+
+typedef void (*ukern)(uint64_t*, uint32_t*, int);
+
+static double run_issue(ukern k, int instr_per_iter, int iters, int threads) {
+  uint64_t* d_out;
+  uint32_t* d_sink;
+  CK(hipMalloc(&d_out, 8));
+  CK(hipMalloc(&d_sink, 4 * 1024));
+  hipLaunchKernelGGL(k, dim3(1), dim3(threads), 0, 0, d_out, d_sink, 10);
+  CK(hipDeviceSynchronize());
+  hipLaunchKernelGGL(k, dim3(1), dim3(threads), 0, 0, d_out, d_sink, iters);
+  CK(hipDeviceSynchronize());
+  uint64_t cyc;
+  CK(hipMemcpy(&cyc, d_out, 8, hipMemcpyDeviceToHost));
+  CK(hipFree(d_out));
+  CK(hipFree(d_sink));
+  return (double)cyc / ((double)iters * instr_per_iter);
+}
+
+// ---- 2. MD5 batch kernel -----------------------------------------------------
+static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0) {
+  uint64_t stride = (L + 255) & ~uint64_t(255);
+  uint8_t* d_data;
+  CK(hipMalloc(&d_data, stride * (uint64_t)B));
+  const uint64_t segs = (L + 1023) / 1024;
+  const uint64_t thr = segs * (uint64_t)B;
+  hipLaunchKernelGGL(qsmd5_lcg_fill_kernel, dim3((thr + 255) / 256), dim3(256), 0, 0, d_data,
+                     stride, L, 12345u, (uint32_t)B, segs);
+  std::vector<ChunkDesc> h(B);
+  for (int i = 0; i < B; ++i) {
+    h[i].ptr = d_data + stride * (uint64_t)i;
+    h[i].len = L;
+  }
+  ChunkDesc* d_desc;
+  uint32_t* d_dig;
+  CK(hipMalloc(&d_desc, sizeof(ChunkDesc) * B));
+  CK(hipMalloc(&d_dig, 16 * (size_t)B));
+  CK(hipMemcpy(d_desc, h.data(), sizeof(ChunkDesc) * B, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const int grid = (B + 63) / 64;
+  auto launch = [&]() {
+    if (which == 0)
+      hipLaunchKernelGGL(qsmd5_batch_kernel, dim3(grid), dim3(64), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig);
+    else
+      hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig);
+  };
+  launch();
+  CK(hipGetLastError());
+  CK(hipDeviceSynchronize());
+  std::vector<float> ms(reps);
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0, 0));
+    launch();
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms[r], e0, e1));
+  }
+  float best = ms[0], med;
+  for (float m : ms) best = m < best ? m : best;
+  std::vector<float> s = ms;
+  std::sort(s.begin(), s.end());
+  med = s[s.size() / 2];
+  double gib = (double)L * B / (1u << 30);
+  printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
+         "%.1f cycles/block @2.4GHz\n",
+         which ? "pc" : "v1", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         (med / 1e3) * 2.4e9 / (double)(L / 64));
+  if (check) {
+    std::vector<uint32_t> dig(4 * (size_t)B);
+    CK(hipMemcpy(dig.data(), d_dig, 16 * (size_t)B, hipMemcpyDeviceToHost));
+    std::vector<uint8_t> host(L);
+    int bad = 0;
+    int ncheck = B < 16 ? B : 16;
+    for (int i = 0; i < ncheck; ++i) {
+      int ci = (i * 7919) % B;
+      CK(hipMemcpy(host.data(), d_data + stride * (uint64_t)ci, L, hipMemcpyDeviceToHost));
+      std::vector<uint8_t> ref(L);
+      oracle_lcg_fill(ref.data(), L, 12345u + ci);
+      if (memcmp(ref.data(), host.data(), L) != 0) {
+        printf("  generator mismatch chunk %d\n", ci);
+        ++bad;
+      }
+      uint8_t od[16];
+      oracle_md5(host.data(), L, od);
+      if (memcmp(od, &dig[4 * (size_t)ci], 16) != 0) {
+        char hx[33], hg[33];
+        oracle_md5_hex(od, hx);
+        oracle_md5_hex((const uint8_t*)&dig[4 * (size_t)ci], hg);
+        printf("  DIGEST MISMATCH chunk %d: oracle %s gpu %s\n", ci, hx, hg);
+        ++bad;
+      }
+    }
+    printf("  check %d chunks: %s\n", ncheck, bad ? "FAIL" : "ok");
+  }
+  CK(hipFree(d_data));
+  CK(hipFree(d_desc));
+  CK(hipFree(d_dig));
+}
+
+// Edge lengths on unaligned offsets, 1 launch each, all checked.
+static int run_edges(int which) {
+  const uint64_t lens[] = {0, 1, 3, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 1000, 4096, 8191, 100003};
+  const int nl = sizeof(lens) / sizeof(lens[0]);
+  int bad = 0;
+  uint8_t* d;
+  CK(hipMalloc(&d, 1 << 20));
+  std::vector<uint8_t> h(1 << 20);
+  oracle_lcg_fill(h.data(), h.size(), 777u);
+  CK(hipMemcpy(d, h.data(), h.size(), hipMemcpyHostToDevice));
+  std::vector<ChunkDesc> desc;
+  std::vector<std::pair<uint64_t, uint64_t>> ref;
+  for (int off = 0; off < 8; ++off)
+    for (int i = 0; i < nl; ++i) {
+      uint64_t o = off * 4099 + off;
+      desc.push_back({d + o, lens[i]});
+      ref.push_back({o, lens[i]});
+    }
+  int n = desc.size();
+  ChunkDesc* dd;
+  uint32_t* dg;
+  CK(hipMalloc(&dd, sizeof(ChunkDesc) * n));
+  CK(hipMalloc(&dg, 16 * n));
+  CK(hipMemcpy(dd, desc.data(), sizeof(ChunkDesc) * n, hipMemcpyHostToDevice));
+  CK(hipMemset(dg, 0, 16 * n));
+  if (which == 0)
+    hipLaunchKernelGGL(qsmd5_batch_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, dd, nullptr,
+                       (uint32_t)n, dg);
+  else
+    hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
+                       (uint32_t)n, dg);
+  CK(hipDeviceSynchronize());
+  std::vector<uint8_t> got(16 * n);
+  CK(hipMemcpy(got.data(), dg, 16 * n, hipMemcpyDeviceToHost));
+  for (int i = 0; i < n; ++i) {
+    uint8_t od[16];
+    oracle_md5(h.data() + ref[i].first, ref[i].second, od);
+    if (memcmp(od, &got[16 * i], 16)) {
+      printf("  edge mismatch off=%llu len=%llu\n", (unsigned long long)ref[i].first,
+             (unsigned long long)ref[i].second);
+      ++bad;
+    }
+  }
+  printf("edges[%d]: %d cases, %d bad\n", which, n, bad);
+  CK(hipFree(d));
+  CK(hipFree(dd));
+  CK(hipFree(dg));
+  return bad;
+}
+
+int main(int argc, char** argv) {
+  int dev = 0;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, dev));
+  printf("device %s %s CUs=%d clock=%d kHz\n", prop.name, prop.gcnArchName,
+         prop.multiProcessorCount, prop.clockRate);
+  const int iters = 20000;
+  printf("issue (cycles/instr, s_memtime ticks, 1 wave):\n");
+  printf("  dep v_add_u32      %.2f\n", run_issue(k_dep_add, 64, iters, 64));
+  printf("  ind v_add_u32 x4   %.2f\n", run_issue(k_ind_add, 256, iters, 64));
+  printf("  dep v_alignbit     %.2f\n", run_issue(k_dep_alignbit, 64, iters, 64));
+  printf("  dep v_bitop3       %.2f\n", run_issue(k_dep_bitop3, 64, iters, 64));
+  printf("  dep v_add3_u32     %.2f\n", run_issue(k_dep_add3, 64, iters, 64));
+  printf("  md5 step (5 ins)   %.2f per instr\n", run_issue(k_md5_step, 320, iters, 64));
+  printf("  md5 step4 (4 ins)  %.2f per instr\n", run_issue(k_md5_step4, 256, iters, 64));
+  printf("  dep v_add_u32 2 waves/WG   %.2f\n", run_issue(k_dep_add, 64, iters, 128));
+  printf("  dep v_add_u32 8 waves/WG   %.2f\n", run_issue(k_dep_add, 64, iters, 512));
+  printf("  dep v_add_u32 16 waves/WG  %.2f\n", run_issue(k_dep_add, 64, iters, 1024));
+  int bad = run_edges(0) + run_edges(1);
+  const uint64_t L = 10485760;
+  for (int w = 0; w < 2; ++w) {
+    run_md5(1, L, 3, true, w);
+    run_md5(512, L, 5, true, w);
+    run_md5(4096, L, 3, true, w);
+    run_md5(65536, 65536, 5, true, w);
+  }
+  run_md5(512, 1 << 20, 5, true, 1);
+  run_md5(4096, 1 << 20, 5, true, 1);
+  run_md5(262144, 16384, 5, true, 0);
+  return bad ? 1 : 0;
+}
