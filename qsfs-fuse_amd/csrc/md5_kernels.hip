@@ -100,7 +100,9 @@ __device__ __forceinline__ void blocks_unaligned(uint32_t (&st)[4], const uint8_
 }
 
 // Final 1 or 2 blocks: the rem (< 64) trailing bytes, 0x80, zero fill, and the
-// 64-bit little-endian bit count (MD5.cpp:282-312).
+// 64-bit little-endian bit count (MD5.cpp:282-312).  Only dwords holding at
+// least one of the rem bytes are read (none when rem == 0), so an empty or
+// short tail never touches memory outside the message.
 __device__ __forceinline__ void finish(uint32_t (&st)[4], const uint8_t* tp, uint32_t rem,
                                        uint64_t total_len) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(tp);
@@ -108,7 +110,8 @@ __device__ __forceinline__ void finish(uint32_t (&st)[4], const uint8_t* tp, uin
   const uint32_t off = static_cast<uint32_t>(a & 3u);
   uint32_t d[17];
 #pragma unroll
-  for (int k = 0; k < 17; ++k) d[k] = (uint32_t)(4 * k) < off + rem ? load4(base + k) : 0u;
+  for (int k = 0; k < 17; ++k)
+    d[k] = (rem != 0u && (uint32_t)(4 * k) < off + rem) ? load4(base + k) : 0u;
   uint32_t w[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {

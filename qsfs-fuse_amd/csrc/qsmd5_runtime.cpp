@@ -267,7 +267,7 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   if (int rc = r.d_dig.reserve(n * 16 + 16)) return rc;
   qsmd5_chunk* hd = static_cast<qsmd5_chunk*>(r.h_desc.p);
   uint32_t* ho = static_cast<uint32_t*>(r.h_order.p);
-  for (size_t i = 0; i < n; ++i) hd[i] = {chunks[i].ptr, len[i]};
+  for (size_t i = 0; i < n; ++i) hd[i] = {len[i] ? chunks[i].ptr : nullptr, len[i]};
   uint8_t* stage = static_cast<uint8_t*>(r.d_staging.p);
   std::vector<std::vector<uint64_t>> stage_off(slices.size());
   for (size_t si = 0; si < slices.size(); ++si) {

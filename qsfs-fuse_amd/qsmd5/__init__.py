@@ -63,6 +63,14 @@ def lib():
     path = lib_path()
     if not os.path.exists(path):
         raise OSError("libqsmd5.so not built at %s (run __graft_entry__.build())" % path)
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64.so.7.
+    # Loading torch first lets libqsmd5's NEEDED libamdhip64.so.7 bind to that
+    # copy instead of pulling /opt/rocm's in beside it (two runtimes in one
+    # process leave torch without devices).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(path)
     c_u8p = ctypes.POINTER(ctypes.c_uint8)
     sig = {

@@ -136,8 +136,9 @@ def test_strerror():
     assert L.qsmd5_strerror(-errno.ENODEV) == b"no usable GPU"
 
 
-@pytest.mark.skipif(qsmd5.device_count() > 0, reason="GPU present")
 def test_no_gpu_fails_loudly():
+    if qsmd5.device_count() > 0:
+        pytest.skip("GPU present")
     with pytest.raises(qsmd5.Md5Error) as e:
         qsmd5.hash_one(b"abc")
     assert e.value.code == -errno.ENODEV
