@@ -7,11 +7,16 @@
 // kernel set in md5_kernels.hip.
 //
 // Host-resident batches (the qsfs case: parts sit in pooled host buffers,
-// ResourceManager.cpp:53-77) are cut into slices of about kSliceBytes; each
-// slice is copied H2D into a ring region on the copy stream and hashed by its
-// own launch on one of kComputeStreams streams, so PCIe transfer of slice k+1
-// overlaps hashing of slice k and slice kernels run concurrently (each one is
-// latency-bound on a handful of CUs).
+// ResourceManager.cpp:53-77) are cut into slices (a quarter of the batch,
+// clamped to [512 MiB, 4 GiB]); each slice is copied H2D into a ring region on
+// the copy stream and hashed by its own launch on one of kComputeStreams
+// streams, so PCIe transfer of slice k+1 overlaps hashing of slice k.  A slice
+// launch takes one chain time (~85 ms for 10 MiB parts) whatever its size and
+// only ~4 hardware queues run kernels concurrently, so slices are kept large
+// enough that the copy, not kernel concurrency, is the bound.  Staged chunks
+// are packed with a 4 KiB + 256 B skew so that equal-size parts never sit at a
+// power-of-two stride (lanes walk their chunks in lockstep; a power-of-two
+// stride sends every lane's request to the same HBM channel).
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -36,9 +41,13 @@ using qsmd5::kKernelThroughput;
 
 constexpr uint64_t kMaxChunkLen = 1ull << 38;
 constexpr int kComputeStreams = 8;
-constexpr uint64_t kSliceBytes = 1ull << 30;        // ~1 GiB per H2D slice
+constexpr uint64_t kSliceMin = 512ull << 20;        // H2D slice bounds
+constexpr uint64_t kSliceMax = 4ull << 30;
 constexpr uint64_t kDefaultStaging = 16ull << 30;   // device staging ring
 constexpr uint64_t kAlign = 256;
+constexpr uint64_t kSkew = 4096 + 256;
+
+inline uint64_t stage_bytes(uint64_t L) { return ((L + kAlign - 1) & ~(kAlign - 1)) + kSkew; }
 
 thread_local std::string t_last_error;
 
@@ -224,7 +233,7 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
     kind[i] = L ? classify(chunks[i].ptr) : kDeviceMem;  // empty chunks read nothing
     if (kind[i] == kHostMem) {
       max_host = std::max(max_host, L);
-      host_total += (L + kAlign - 1) & ~(kAlign - 1);
+      host_total += stage_bytes(L);
     }
   }
 
@@ -237,12 +246,14 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   std::sort(host_idx.begin(), host_idx.end(), by_len);
 
   // Slices of host chunks and their staging regions.
-  const uint64_t region = std::max<uint64_t>(kSliceBytes, (max_host + kAlign - 1) & ~(kAlign - 1));
+  const uint64_t slice_target = env_u64(
+      "QSMD5_SLICE_BYTES", std::min(kSliceMax, std::max(kSliceMin, host_total / 4)));
+  const uint64_t region = std::max<uint64_t>(slice_target, stage_bytes(max_host));
   std::vector<Slice> slices;
   for (size_t k = 0; k < host_idx.size();) {
     Slice s{k, 0, 0};
     while (k < host_idx.size()) {
-      uint64_t L = (len[host_idx[k]] + kAlign - 1) & ~(kAlign - 1);
+      uint64_t L = stage_bytes(len[host_idx[k]]);
       if (s.count > 0 && s.bytes + L > region) break;
       s.bytes += L;
       ++s.count;
@@ -277,7 +288,7 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
       uint32_t ci = host_idx[slices[si].first + k];
       hd[ci].ptr = base + off;
       stage_off[si].push_back(off);
-      off += (len[ci] + kAlign - 1) & ~(kAlign - 1);
+      off += stage_bytes(len[ci]);
     }
   }
   size_t pos = 0;

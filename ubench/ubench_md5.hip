@@ -151,8 +151,8 @@ static double run_issue(ukern k, int instr_per_iter, int iters, int threads) {
 }
 
 // ---- 2. MD5 batch kernel -----------------------------------------------------
-static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0) {
-  uint64_t stride = (L + 255) & ~uint64_t(255);
+static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint64_t pad = 0) {
+  uint64_t stride = ((L + 255) & ~uint64_t(255)) + pad;
   uint8_t* d_data;
   CK(hipMalloc(&d_data, stride * (uint64_t)B));
   const uint64_t segs = (L + 1023) / 1024;
@@ -198,6 +198,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0) {
   std::sort(s.begin(), s.end());
   med = s[s.size() / 2];
   double gib = (double)L * B / (1u << 30);
+  if (pad) printf("(stride pad %llu) ", (unsigned long long)pad);
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
          which ? "pc" : "v1", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
@@ -284,7 +285,74 @@ static int run_edges(int which) {
   return bad;
 }
 
+// Coalesced streaming read (16 B/lane, grid-stride): the FETCH_SIZE calibration
+// reference of MI355X_MICROARCH.md §HBM and the achievable HBM read rate here.
+__global__ __launch_bounds__(256) void k_stream_read(const u32x4* __restrict__ p, uint64_t n16,
+                                                     uint32_t* sink) {
+  u32x4 acc = {0, 0, 0, 0};
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n16;
+       i += (uint64_t)gridDim.x * 256) {
+    u32x4 v = __builtin_nontemporal_load(p + i);
+    acc ^= v;
+  }
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1;
+}
+
+static void run_stream_read(uint64_t bytes, int reps) {
+  u32x4* d;
+  uint32_t* sink;
+  CK(hipMalloc(&d, bytes));
+  CK(hipMalloc(&sink, 4));
+  CK(hipMemset(d, 1, bytes));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float best = 1e30f;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(k_stream_read, dim3(256 * 8), dim3(256), 0, 0, d, bytes / 16, sink);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    best = ms < best ? ms : best;
+  }
+  printf("stream_read %llu bytes: best %.3f ms -> %.1f GB/s\n", (unsigned long long)bytes, best,
+         bytes / (best * 1e-3) / 1e9);
+  CK(hipFree(d));
+  CK(hipFree(sink));
+}
+
 int main(int argc, char** argv) {
+  const char* mode = argc > 1 ? argv[1] : "all";
+  if (!strcmp(mode, "calib")) {
+    // one launch each, for rocprofv3 --pmc FETCH_SIZE
+    run_stream_read(4ull << 30, 2);
+    run_md5(512, 10485760, 1, false, 1);
+    run_md5(131072, 65536, 1, false, 0);
+    return 0;
+  }
+  if (!strcmp(mode, "stride")) {
+    for (uint64_t mib : {10ull, 16ull, 32ull, 64ull}) {
+      run_md5(512, mib << 20, 2, false, 1, 0);
+      run_md5(512, mib << 20, 2, false, 1, 4096);
+      run_md5(512, mib << 20, 2, false, 1, 65536 + 256);
+    }
+    run_md5(512, 32ull << 20, 2, false, 0, 0);
+    run_md5(512, 32ull << 20, 2, false, 0, 4096);
+    return 0;
+  }
+  if (!strcmp(mode, "sat")) {
+    run_stream_read(8ull << 30, 5);
+    run_md5(131072, 65536, 5, true, 0, 0);
+    run_md5(131072, 65536, 5, true, 0, 4352);
+    run_md5(262144, 32768, 5, true, 0, 4352);
+    run_md5(524288, 16384, 5, true, 0, 4352);
+    run_md5(65536, 262144, 3, true, 0, 4352);
+    run_md5(16384, 1 << 20, 3, true, 1, 4352);
+    run_md5(512, 10485760, 3, true, 0, 0);
+    return 0;
+  }
   int dev = 0;
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, dev));
