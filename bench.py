@@ -132,6 +132,8 @@ def main():
     ap.add_argument("--batch", type=int, default=BATCH, help="chunks per GPU (default 512)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="N>1 rehearsal on a 1-GPU box: every rank on cuda:0, gloo digest gather")
     args = ap.parse_args()
 
     import torch
@@ -146,11 +148,16 @@ def main():
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (the MD5 path has no CPU fallback)")
+    if args.rehearse_gloo:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if args.rehearse_gloo:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
     rc = qsmd5.lib().qsmd5_init(0)
     if rc != 0:
         raise SystemExit("qsmd5_init failed: %d" % rc)
@@ -199,7 +206,8 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64,
+                          device="cpu" if args.rehearse_gloo else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     kernel_ms = [a.elapsed_time(b) for a, b in events]

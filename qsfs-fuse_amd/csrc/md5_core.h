@@ -97,16 +97,16 @@ __device__ __forceinline__ void md5_steps(uint32_t (&v)[4], const uint32_t (&w)[
 // Steps with the message-and-constant term mk[i] = x[word(i)] + K[i] supplied
 // precomputed (by the producer wave of qsmd5_batch_pc_kernel): each step is then
 // exactly v_bitop3 + v_add3 + v_alignbit + v_add.
-template <int I>
+template <int I, int kEnd = 64>
 __device__ __forceinline__ void md5_steps_mk(uint32_t (&v)[4], const uint32_t (&mk)[64]) {
-  if constexpr (I < 64) {
+  if constexpr (I < kEnd) {
     constexpr int ia = (4 - (I & 3)) & 3;
     constexpr int ib = (ia + 1) & 3;
     constexpr int ic = (ia + 2) & 3;
     constexpr int id = (ia + 3) & 3;
     const uint32_t t = v[ia] + md5_round_fn<I>(v[ib], v[ic], v[id]) + mk[I];
     v[ia] = v[ib] + __builtin_rotateleft32(t, md5_shift(I));
-    md5_steps_mk<I + 1>(v, mk);
+    md5_steps_mk<I + 1, kEnd>(v, mk);
   }
 }
 

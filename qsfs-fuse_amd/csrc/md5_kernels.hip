@@ -153,6 +153,12 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return v;
 }
 
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+
 // LDS-only workgroup barrier: wait for this wave's LDS traffic, then s_barrier.
 // Deliberately not __syncthreads(): its fence would also drain vmcnt and kill
 // the producer's global-load prefetch that spans the barrier.
@@ -202,6 +208,39 @@ __device__ __forceinline__ void pc_write_mk(u32x4 (*slot)[64], uint32_t lane, co
     slot[g][lane] = m;
   }
 }
+
+
+// One phase of the chain wave: kPcHalf blocks from ring slots s0.., the
+// operands of block h+1 read from LDS while block h compresses.  kAllLive
+// drops the per-block lane predicate (every lane has blocks blk0..blk0+H-1).
+template <bool kAllLive>
+__device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*ring)[16][64],
+                                            uint32_t s0, uint32_t lane, uint32_t blk0,
+                                            uint32_t nblk) {
+  u32x4 a[16], b[16];
+  auto read_slot = [&](u32x4 (&dst)[16], uint32_t slot) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dst[g] = ring[slot][g][lane];
+  };
+  auto compress_slot = [&](const u32x4 (&src)[16]) {
+    uint32_t mk[64];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      mk[4 * g + 0] = src[g].x;
+      mk[4 * g + 1] = src[g].y;
+      mk[4 * g + 2] = src[g].z;
+      mk[4 * g + 3] = src[g].w;
+    }
+    md5_compress_mk(st, mk);
+  };
+  read_slot(a, s0);
+#pragma unroll
+  for (int h = 0; h < kPcHalf; ++h) {
+    if (h + 1 < kPcHalf) read_slot((h & 1) ? a : b, s0 + h + 1);
+    if (kAllLive || blk0 + h < nblk) compress_slot((h & 1) ? b : a);
+  }
+}
+
 
 }  // namespace qsmd5
 
@@ -307,7 +346,8 @@ extern "C" __global__ __launch_bounds__(256) void qsmd5_lcg_fill_kernel(
   }
 }
 
-// Latency-regime batch kernel (B up to ~64 K chunks): see qsmd5::kPcHalf notes.
+// Latency-regime batch kernel (B up to one resident round, 256 x 64 chunks):
+// see the producer/consumer notes at kPcHalf.
 extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
     uint32_t* __restrict__ digests) {
@@ -361,36 +401,18 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
   }
 
   // ---------------- chain ----------------
+  // Phases in which every live lane still has all kPcHalf blocks run without a
+  // per-block lane predicate (wave-uniform branch on an SGPR).
+  const uint32_t live_phases = __builtin_amdgcn_readfirstlane(
+      wave_min_u32(t < n ? nblk : 0xffffffffu) / kPcHalf);
   uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
   lds_barrier();
   for (uint32_t p = 0; p < phases; ++p) {
     const uint32_t s0 = (p & 1u) * kPcHalf;
-    u32x4 cur[16];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) cur[g] = ring[s0][g][lane];
-#pragma unroll
-    for (int h = 0; h < kPcHalf; ++h) {
-      u32x4 nxt[16];
-      if (h + 1 < kPcHalf) {
-#pragma unroll
-        for (int g = 0; g < 16; ++g) nxt[g] = ring[s0 + h + 1][g][lane];
-      }
-      if (p * kPcHalf + h < nblk) {
-        uint32_t mk[64];
-#pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          mk[4 * g + 0] = cur[g].x;
-          mk[4 * g + 1] = cur[g].y;
-          mk[4 * g + 2] = cur[g].z;
-          mk[4 * g + 3] = cur[g].w;
-        }
-        md5_compress_mk(st, mk);
-      }
-      if (h + 1 < kPcHalf) {
-#pragma unroll
-        for (int g = 0; g < 16; ++g) cur[g] = nxt[g];
-      }
-    }
+    if (p < live_phases)
+      chain_phase<true>(st, ring, s0, lane, p * kPcHalf, nblk);
+    else
+      chain_phase<false>(st, ring, s0, lane, p * kPcHalf, nblk);
     lds_barrier();
   }
   if (t >= n) return;

@@ -32,11 +32,14 @@ def gather_digests(local, n, group=None):
         raise ValueError("local digests must be [m, 16]")
     pad = torch.zeros((m_max, 16), dtype=torch.uint8, device=local.device)
     pad[: local.shape[0]] = local
-    out = torch.empty((world * m_max, 16), dtype=torch.uint8, device=local.device)
     if dist.get_backend(group) == "gloo":
-        parts = list(out.chunk(world))
-        dist.all_gather(parts, pad, group=group)
+        # gloo (CPU tests, single-GPU rehearsals) gathers host tensors
+        pad_h = pad.cpu()
+        parts = [torch.empty_like(pad_h) for _ in range(world)]
+        dist.all_gather(parts, pad_h, group=group)
+        out = torch.cat(parts, 0).to(local.device)
     else:
+        out = torch.empty((world * m_max, 16), dtype=torch.uint8, device=local.device)
         dist.all_gather_into_tensor(out, pad, group=group)
     rows = [out[r * m_max: r * m_max + (e - b)] for r, (b, e) in enumerate(sizes)]
     return torch.cat(rows, 0)

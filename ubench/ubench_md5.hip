@@ -132,6 +132,25 @@ __global__ void k_md5_step4(uint64_t* out, uint32_t* sink, int iters) {
   sink[threadIdx.x] = a + b + c + d;
 }
 
+// VALU + ds_read_b128 interleaved (1 LDS read per 4 VALU, as the chain wave).
+__global__ void k_mix_lds(uint64_t* out, uint32_t* sink, int iters) {
+  __shared__ u32x4 lds[64];
+  lds[threadIdx.x] = u32x4{threadIdx.x, 1, 2, 3};
+  __syncthreads();
+  uint32_t v0 = threadIdx.x, v1 = 3;
+  u32x4 r;
+  uint32_t addr = threadIdx.x * 16;
+  uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    asm volatile(REP64("ds_read_b128 %2, %3\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n v_add_u32 %0, %0, %1\n")
+                 : "+v"(v0), "+v"(v1), "=&v"(r) : "v"(addr));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) out[0] = t1 - t0;
+  sink[threadIdx.x] = v0 + r.x;
+}
+
 typedef void (*ukern)(uint64_t*, uint32_t*, int);
 
 static double run_issue(ukern k, int instr_per_iter, int iters, int threads) {
@@ -332,6 +351,22 @@ int main(int argc, char** argv) {
     run_md5(131072, 65536, 1, false, 0);
     return 0;
   }
+  if (!strcmp(mode, "ab")) {
+    int bad = run_edges(0) + run_edges(1);
+    for (int r = 0; r < 3; ++r) {
+      run_md5(512, 10485760, 3, r == 0, 0);
+      run_md5(512, 10485760, 3, r == 0, 1);
+    }
+    run_md5(600, 1 << 20, 3, true, 1);
+    run_md5(4096, 1 << 20, 3, true, 1);
+    return bad ? 1 : 0;
+  }
+  if (!strcmp(mode, "issue")) {
+    const int iters = 20000;
+    printf("  dep v_add_u32      %.2f\n", run_issue(k_dep_add, 64, iters, 64));
+    printf("  4 v_add + ds_read  %.2f per group\n", run_issue(k_mix_lds, 64, iters, 64));
+    return 0;
+  }
   if (!strcmp(mode, "stride")) {
     for (uint64_t mib : {10ull, 16ull, 32ull, 64ull}) {
       run_md5(512, mib << 20, 2, false, 1, 0);
@@ -367,6 +402,7 @@ int main(int argc, char** argv) {
   printf("  dep v_add3_u32     %.2f\n", run_issue(k_dep_add3, 64, iters, 64));
   printf("  md5 step (5 ins)   %.2f per instr\n", run_issue(k_md5_step, 320, iters, 64));
   printf("  md5 step4 (4 ins)  %.2f per instr\n", run_issue(k_md5_step4, 256, iters, 64));
+  printf("  4 v_add + ds_read  %.2f per group\n", run_issue(k_mix_lds, 64, iters, 64));
   printf("  dep v_add_u32 2 waves/WG   %.2f\n", run_issue(k_dep_add, 64, iters, 128));
   printf("  dep v_add_u32 8 waves/WG   %.2f\n", run_issue(k_dep_add, 64, iters, 512));
   printf("  dep v_add_u32 16 waves/WG  %.2f\n", run_issue(k_dep_add, 64, iters, 1024));
