@@ -191,7 +191,8 @@ def saturation(reps):
           for _ in range(reps + 1)]
     for a, b in ev:
         a.record(s)
-        qsmd5.hash_device(desc.data_ptr(), dig.data_ptr(), n, stream=s.cuda_stream)
+        qsmd5.hash_device(desc.data_ptr(), dig.data_ptr(), n, stream=s.cuda_stream,
+                          flags=qsmd5.FLAG_ALIGNED16)
         b.record(s)
     torch.cuda.synchronize()
     ms = min(a.elapsed_time(b) for a, b in ev[1:])
@@ -200,7 +201,7 @@ def saturation(reps):
     ok = [bytes(r) for r in dig[:64].cpu().numpy()] == want
     gbs = n * L / (ms * 1e-3) / 1e9
     emit({"config": "saturation", "workload": "%d x 64 KiB device-resident, stride 64 KiB + 4352 B (kernel %s)" % (
-        n, "pc" if qsmd5.kernel_choice(n) == 1 else "v1"),
+        n, ["v1", "pc", "coal"][qsmd5.kernel_choice(n, qsmd5.FLAG_ALIGNED16)]),
         "GiBps": round(n * L / GiB / (ms * 1e-3), 1), "GBps": round(gbs, 1),
         "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "kernel_ms": round(ms, 3),
         "parity": "ok (64 sampled chunks vs oracle)" if ok else "FAIL"})

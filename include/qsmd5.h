@@ -73,6 +73,7 @@ typedef struct qsmd5_part {
 /* Flags for qsmd5_init / qsmd5_hash_batch_ex. */
 #define QSMD5_FLAG_NONE 0
 #define QSMD5_FLAG_REF_TRUNCATE32 1 /* hash only len mod 2^32 bytes, like MD5(std::string) */
+#define QSMD5_FLAG_ALIGNED16 2      /* device_async_ex: caller promises 16-B-aligned chunk ptrs */
 
 /* Initialise the runtime on the current HIP device (idempotent).  Returns 0,
  * or -ENODEV when no GPU is usable. */
@@ -112,10 +113,19 @@ QSMD5_API int qsmd5_hash_batch_ex(const qsmd5_chunk* chunks, size_t n, uint8_t (
 QSMD5_API int qsmd5_hash_batch_device_async(const qsmd5_chunk* d_chunks, const uint32_t* d_order, size_t n,
                                   uint8_t (*d_digests)[16], void* hip_stream);
 
-/* Which kernel qsmd5_hash_batch_device_async launches for a batch of n
- * chunks: 1 = producer/consumer latency kernel, 0 = one-wave throughput
- * kernel.  QSMD5_KERNEL env ("pc"/"v1") overrides. */
+/* As qsmd5_hash_batch_device_async; flags may carry QSMD5_FLAG_ALIGNED16,
+ * which lets batches beyond one resident round (> 16 384 chunks) use the
+ * coalesced LDS-DMA throughput kernel. */
+QSMD5_API int qsmd5_hash_batch_device_async_ex(const qsmd5_chunk* d_chunks, const uint32_t* d_order,
+                                     size_t n, uint8_t (*d_digests)[16], void* hip_stream,
+                                     int flags);
+
+/* Which kernel a device batch of n chunks gets: 1 = producer/consumer latency
+ * kernel (n <= 16 384), 2 = coalesced throughput kernel (larger, 16-B-aligned
+ * chunks), 0 = one-wave throughput kernel (larger, any alignment).
+ * QSMD5_KERNEL env ("pc"/"coal"/"v1") overrides. */
 QSMD5_API int qsmd5_kernel_choice(size_t n);
+QSMD5_API int qsmd5_kernel_choice_ex(size_t n, int flags);
 
 /* Lowercase hex, exactly MD5::hexdigest()'s "%02x" x 16 (MD5.cpp:317-325);
  * out must hold 33 bytes (NUL-terminated).  Host-only, needs no GPU. */

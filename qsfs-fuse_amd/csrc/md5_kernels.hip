@@ -422,6 +422,118 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Throughput kernel with coalesced LDS-DMA staging (batches of >> 16 K chunks).
+//
+// Each lane walking its own chunk makes every load instruction touch 64
+// different lines; that pattern alone tops out at ~4.0-4.6 TB/s on MI355X
+// (ubench lane_stream) against 7.1 TB/s for coalesced reads.  Here the wave
+// instead stages 2 blocks (128 B) of each of its 64 chains per tile with 8
+// global_load_lds_dwordx4: instruction i fetches chains 8i..8i+7, 8 lanes x 16 B
+// contiguous per chain, straight into LDS rows [chain][8 x 16 B].  Each lane
+// then reads its own row back (8 ds_read_b128).  The 16-B slots of row c are
+// XOR-swizzled by (c >> 1) & 7 on the SOURCE address (the LDS-DMA destination
+// is lane-linear), which makes the row reads bank-conflict-free.  Tiles are
+// double-buffered: tile t+1 is in flight (vmcnt 8) while tile t compresses.
+// Requires 16-byte-aligned chunks (the host routes others to qsmd5_batch_kernel).
+#define QS_GP(p) ((const __attribute__((address_space(1))) void*)(uintptr_t)(p))
+#define QS_LP(p) ((__attribute__((address_space(3))) void*)(uintptr_t)(uint32_t)(uintptr_t)(p))
+
+template <int kBufs>
+__device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ chunks,
+                                                const uint32_t* __restrict__ order, uint32_t n,
+                                                uint32_t* __restrict__ digests) {
+  // kBufs tile buffers: kBufs - 1 tiles in flight while one compresses.
+  __shared__ u32x4 tile_buf[kBufs][64][8];
+  const uint32_t lane = threadIdx.x;
+  const uint32_t t = blockIdx.x * 64u + lane;
+  uint32_t idx = 0;
+  ChunkDesc cd = {nullptr, 0};
+  if (t < n) {
+    idx = order ? order[t] : t;
+    cd = chunks[idx];
+  }
+  const uint32_t nblk = (uint32_t)(cd.len >> 6);
+  const uint32_t ntiles = (wave_max_u32(nblk) + 1u) >> 1;
+
+  // Loader role of this lane in instruction i: chain 8i + (lane >> 3), slot lane & 7.
+  const uint32_t slot = lane & 7u;
+  const uint64_t myptr = reinterpret_cast<uint64_t>(cd.ptr);
+  const uint8_t* src[8];
+  uint32_t src_nblk[8], piece[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = i * 8 + (int)(lane >> 3);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)myptr, c, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(myptr >> 32), c, 64);
+    src[i] = reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo);
+    src_nblk[i] = (uint32_t)__shfl((int)nblk, c, 64);
+    piece[i] = slot ^ (((uint32_t)c >> 1) & 7u);  // 16-B piece this lane fetches
+  }
+  auto issue_tile = [&](uint32_t b, uint32_t tl) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (src_nblk[i]) {
+        const uint32_t blk = min(tl * 2u + (piece[i] >> 2), src_nblk[i] - 1u);
+        const uint8_t* g = src[i] + (uint64_t)blk * 64u + (piece[i] & 3u) * 16u;
+        __builtin_amdgcn_global_load_lds(QS_GP(g), QS_LP(&tile_buf[b][i * 8][0]), 16, 0, 0);
+      }
+    }
+  };
+  const uint32_t rswz = (lane >> 1) & 7u;
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+#pragma unroll
+  for (int k = 0; k < kBufs - 1; ++k)
+    if ((uint32_t)k < ntiles) issue_tile((uint32_t)k, (uint32_t)k);
+  for (uint32_t tl = 0; tl < ntiles; ++tl) {
+    const uint32_t b = tl % kBufs;
+    if (tl + (kBufs - 1) < ntiles) {
+      issue_tile((tl + (kBufs - 1)) % kBufs, tl + (kBufs - 1));
+      // the kBufs - 1 younger tiles (8 LDS-DMA each) may stay in flight
+      if constexpr (kBufs == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      // tail: fewer tiles follow; drain (rare, last kBufs - 1 tiles only)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    u32x4 q[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q[k] = tile_buf[b][lane][k ^ rswz];
+    uint32_t w[16];
+    if (tl * 2u < nblk) {
+      unpack4(w, 0, q[0]);
+      unpack4(w, 1, q[1]);
+      unpack4(w, 2, q[2]);
+      unpack4(w, 3, q[3]);
+      md5_compress(st, w);
+    }
+    if (tl * 2u + 1u < nblk) {
+      unpack4(w, 0, q[4]);
+      unpack4(w, 1, q[5]);
+      unpack4(w, 2, q[6]);
+      unpack4(w, 3, q[7]);
+      md5_compress(st, w);
+    }
+    // the next issue_tile may overwrite a buffer: make sure the row reads are done
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (t >= n) return;
+  finish(st, cd.ptr + ((uint64_t)nblk << 6), (uint32_t)(cd.len & 63u), cd.len);
+  u32x4 o = {st[0], st[1], st[2], st[3]};
+  *reinterpret_cast<u32x4*>(digests + 4u * (uint64_t)idx) = o;
+}
+// Two tile buffers (16 KiB LDS per wave, up to 10 waves per CU): a third
+// buffer measured slower at 131072 x 64 KiB (24 KiB per wave cuts residency to
+// 6 waves per CU and the batch no longer fits one round).
+extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_coal_kernel(
+    const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
+    uint32_t* __restrict__ digests) {
+  batch_coal_body<2>(chunks, order, n, digests);
+}
+
+#undef QS_GP
+#undef QS_LP
+
+// ---------------------------------------------------------------------------
 // Host launchers (md5_launch.h).
 #include "md5_launch.h"
 
@@ -433,6 +545,9 @@ hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, u
   const uint32_t groups = (n + 63u) / 64u;
   if (kind == kKernelLatency) {
     hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(groups), dim3(128), 0, s,
+                       static_cast<const ChunkDesc*>(chunks), order, n, digests);
+  } else if (kind == kKernelCoalesced) {
+    hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3(groups), dim3(64), 0, s,
                        static_cast<const ChunkDesc*>(chunks), order, n, digests);
   } else {
     hipLaunchKernelGGL(qsmd5_batch_kernel, dim3(groups), dim3(64), 0, s,

@@ -10,6 +10,7 @@ namespace qsmd5 {
 enum KernelKind : int {
   kKernelThroughput = 0,  // qsmd5_batch_kernel: 1 wave / 64 chunks, all work in-wave
   kKernelLatency = 1,     // qsmd5_batch_pc_kernel: producer + chain wave / 64 chunks
+  kKernelCoalesced = 2,   // qsmd5_batch_coal_kernel: LDS-DMA coalesced staging, 16-B-aligned
 };
 
 // Chunks one launch of the latency kernel keeps resident at once: one

@@ -36,6 +36,7 @@
 
 namespace {
 
+using qsmd5::kKernelCoalesced;
 using qsmd5::kKernelLatency;
 using qsmd5::kKernelThroughput;
 
@@ -200,13 +201,17 @@ MemKind classify(const void* p) {
   return a.type == hipMemoryTypeDevice ? kDeviceMem : kHostMem;
 }
 
-int kernel_choice(size_t n) {
+int kernel_choice(size_t n, bool aligned16) {
   const char* k = getenv("QSMD5_KERNEL");
   if (k && !strcmp(k, "pc")) return kKernelLatency;
   if (k && !strcmp(k, "v1")) return kKernelThroughput;
+  if (k && !strcmp(k, "coal")) return aligned16 ? kKernelCoalesced : kKernelThroughput;
   // The latency kernel wins while every chunk has its own chain lane in one
-  // resident round; beyond that the one-wave kernel's 2 waves/SIMD win.
-  return n <= qsmd5::kLatencyKernelResident ? kKernelLatency : kKernelThroughput;
+  // resident round (one 128 KiB-LDS workgroup per CU); beyond that the
+  // throughput kernels keep 2+ waves per SIMD and the bound moves to HBM,
+  // where coalesced LDS-DMA staging beats per-lane loads (16-B-aligned chunks).
+  if (n <= qsmd5::kLatencyKernelResident) return kKernelLatency;
+  return aligned16 ? kKernelCoalesced : kKernelThroughput;
 }
 
 struct Slice {
@@ -313,19 +318,23 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   const uint32_t* d_order = static_cast<const uint32_t*>(r.d_order.p);
   uint32_t* d_dig = static_cast<uint32_t*>(r.d_dig.p);
   bool first_kernel = true;
-  auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt) -> int {
+  auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt, bool aligned16) -> int {
     if (first_kernel) {
       QS_HIP(hipEventRecord(k_first, s));
       first_kernel = false;
     }
-    hipError_t e = qsmd5::launch_batch(r.d_desc.p, ord, (uint32_t)cnt, d_dig, kernel_choice(cnt), s);
+    hipError_t e = qsmd5::launch_batch(r.d_desc.p, ord, (uint32_t)cnt, d_dig,
+                                       kernel_choice(cnt, aligned16), s);
     if (e != hipSuccess) return hip_fail(e, "qsmd5 kernel launch");
     return 0;
   };
 
   // Device-resident chunks: one launch.
   if (!dev_idx.empty()) {
-    if ((rc = launch(s0, d_order, dev_idx.size()))) {
+    bool aligned16 = true;
+    for (uint32_t ci : dev_idx)
+      aligned16 = aligned16 && (reinterpret_cast<uintptr_t>(hd[ci].ptr) & 15u) == 0;
+    if ((rc = launch(s0, d_order, dev_idx.size(), aligned16))) {
       cleanup();
       return rc;
     }
@@ -358,7 +367,9 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
       rc = fail(-EIO, "qsmd5: stream wait failed");
       break;
     }
-    if ((rc = launch(cs, d_order + dev_idx.size() + slices[si].first, slices[si].count))) break;
+    // staged chunks sit at 256-B-aligned offsets plus a 16-B-multiple skew
+    if ((rc = launch(cs, d_order + dev_idx.size() + slices[si].first, slices[si].count, true)))
+      break;
     hipEvent_t done;
     if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess ||
         hipEventRecord(done, cs) != hipSuccess) {
@@ -503,18 +514,28 @@ int qsmd5_hash_one(const void* ptr, uint64_t len, uint8_t digest[16]) {
   return qsmd5_hash_batch_ex(&c, 1, reinterpret_cast<uint8_t(*)[16]>(digest), 0);
 }
 
-int qsmd5_kernel_choice(size_t n) { return kernel_choice(n); }
+int qsmd5_kernel_choice(size_t n) { return kernel_choice(n, false); }
+
+int qsmd5_kernel_choice_ex(size_t n, int flags) {
+  return kernel_choice(n, (flags & QSMD5_FLAG_ALIGNED16) != 0);
+}
 
 int qsmd5_hash_batch_device_async(const qsmd5_chunk* d_chunks, const uint32_t* d_order, size_t n,
                                   uint8_t (*d_digests)[16], void* hip_stream) {
+  return qsmd5_hash_batch_device_async_ex(d_chunks, d_order, n, d_digests, hip_stream, 0);
+}
+
+int qsmd5_hash_batch_device_async_ex(const qsmd5_chunk* d_chunks, const uint32_t* d_order,
+                                     size_t n, uint8_t (*d_digests)[16], void* hip_stream,
+                                     int flags) {
   return guarded([&] {
     if (n == 0) return 0;
     if (!d_chunks || !d_digests) return fail(-EINVAL, "qsmd5: NULL device arrays");
     if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
     if (int rc = ensure_init()) return rc;
-    hipError_t e = qsmd5::launch_batch(d_chunks, d_order, (uint32_t)n,
-                                       reinterpret_cast<uint32_t*>(d_digests), kernel_choice(n),
-                                       static_cast<hipStream_t>(hip_stream));
+    hipError_t e = qsmd5::launch_batch(
+        d_chunks, d_order, (uint32_t)n, reinterpret_cast<uint32_t*>(d_digests),
+        kernel_choice(n, (flags & QSMD5_FLAG_ALIGNED16) != 0), static_cast<hipStream_t>(hip_stream));
     if (e != hipSuccess) return hip_fail(e, "qsmd5 kernel launch");
     return 0;
   });

@@ -87,6 +87,10 @@ def lib():
                                                          ctypes.c_size_t, ctypes.c_void_p,
                                                          ctypes.c_void_p]),
         "qsmd5_kernel_choice": (ctypes.c_int, [ctypes.c_size_t]),
+        "qsmd5_kernel_choice_ex": (ctypes.c_int, [ctypes.c_size_t, ctypes.c_int]),
+        "qsmd5_hash_batch_device_async_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p,
+                                                            ctypes.c_size_t, ctypes.c_void_p,
+                                                            ctypes.c_void_p, ctypes.c_int]),
         "qsmd5_hex": (None, [c_u8p, ctypes.c_char_p]),
         "qsmd5_ctx_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
         "qsmd5_ctx_update": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
@@ -129,8 +133,12 @@ def device_count():
     return lib().qsmd5_device_count()
 
 
-def kernel_choice(n):
-    return lib().qsmd5_kernel_choice(n)
+def kernel_choice(n, flags=0):
+    return lib().qsmd5_kernel_choice_ex(n, flags)
+
+
+FLAG_REF_TRUNCATE32 = 1
+FLAG_ALIGNED16 = 2
 
 
 def hexdigest(digest):
@@ -220,12 +228,12 @@ def md5_stream(stream):
     return md5(data)
 
 
-def hash_device(chunks_dev, digests_dev, n, order_dev=None, stream=0):
-    """Enqueue qsmd5_hash_batch_device_async.  chunks_dev: device tensor holding n
-    qsmd5_chunk records (int64 pairs); digests_dev: device uint8 tensor [n,16]."""
-    _check(lib().qsmd5_hash_batch_device_async(
+def hash_device(chunks_dev, digests_dev, n, order_dev=None, stream=0, flags=0):
+    """Enqueue qsmd5_hash_batch_device_async_ex.  chunks_dev: device pointer to n
+    qsmd5_chunk records (int64 pairs); digests_dev: device pointer to [n,16] uint8."""
+    _check(lib().qsmd5_hash_batch_device_async_ex(
         ctypes.c_void_p(int(chunks_dev)), ctypes.c_void_p(int(order_dev or 0)), n,
-        ctypes.c_void_p(int(digests_dev)), ctypes.c_void_p(int(stream or 0))),
+        ctypes.c_void_p(int(digests_dev)), ctypes.c_void_p(int(stream or 0)), flags),
         "qsmd5_hash_batch_device_async")
 
 

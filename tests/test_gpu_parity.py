@@ -32,7 +32,7 @@ def _gpu():
     os.environ.pop("QSMD5_KERNEL", None)
 
 
-@pytest.fixture(params=["pc", "v1"])
+@pytest.fixture(params=["pc", "v1", "coal"])
 def kernel(request):
     os.environ["QSMD5_KERNEL"] = request.param
     yield request.param
@@ -267,6 +267,48 @@ def test_errors_and_empty():
 
 def test_kernel_choice_policy():
     os.environ.pop("QSMD5_KERNEL", None)
-    assert qsmd5.kernel_choice(512) == 1
+    A = qsmd5.FLAG_ALIGNED16
+    assert qsmd5.kernel_choice(512) == 1 and qsmd5.kernel_choice(512, A) == 1
     assert qsmd5.kernel_choice(16384) == 1
     assert qsmd5.kernel_choice(16385) == 0
+    assert qsmd5.kernel_choice(16385, A) == 2
+
+
+def test_coalesced_kernel_ragged_aligned(kernel):
+    """All three kernels on one ragged, 16-B-aligned device batch (lengths 0..~1 MiB)."""
+    import random
+    rng = random.Random(21)
+    lens = [0, 1, 63, 64, 65, 127, 128, 129, 191, 192, 255, 256] + \
+        [rng.randrange(0, 1 << 20) for _ in range(200)]
+    offs, pos = [], 0
+    for L in lens:
+        offs.append(pos)
+        pos += ((L + 15) & ~15) + 16 * rng.randrange(0, 5)
+    t = dev_lcg(99, pos + 64)
+    host = bytes(t.cpu().numpy())
+    hb = (ctypes.c_uint8 * len(host)).from_buffer_copy(host)
+    want = md5_many([(ctypes.addressof(hb) + o, L) for o, L in zip(offs, lens)])
+    got = qsmd5.hash_batch([(t.data_ptr() + o, L) for o, L in zip(offs, lens)])
+    assert got == want
+
+
+def test_coalesced_kernel_device_async_large():
+    """> 16 384 chunks with QSMD5_FLAG_ALIGNED16 goes to the coalesced kernel."""
+    os.environ.pop("QSMD5_KERNEL", None)
+    n, L = 20000, 4096 + 64 + 7
+    S = 8192 + 16
+    t = dev_lcg(3, L, nchunks=n, stride=S)
+    desc = torch.empty((n, 2), dtype=torch.int64)
+    desc[:, 0] = t.data_ptr() + torch.arange(n, dtype=torch.int64) * S
+    desc[:, 1] = L
+    desc = desc.cuda()
+    dig = torch.zeros((n, 16), dtype=torch.uint8, device="cuda")
+    assert qsmd5.kernel_choice(n, qsmd5.FLAG_ALIGNED16) == 2
+    qsmd5.hash_device(desc.data_ptr(), dig.data_ptr(), n,
+                      stream=torch.cuda.current_stream().cuda_stream, flags=qsmd5.FLAG_ALIGNED16)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy()
+    sample = list(range(0, n, 97)) + [n - 1]
+    want = md5_many([(host.ctypes.data + i * S, L) for i in sample])
+    got = [bytes(dig[i].cpu().numpy()) for i in sample]
+    assert got == want

@@ -196,8 +196,11 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     if (which == 0)
       hipLaunchKernelGGL(qsmd5_batch_kernel, dim3(grid), dim3(64), 0, 0, d_desc, nullptr,
                          (uint32_t)B, d_dig);
-    else
+    else if (which == 1)
       hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig);
+    else
+      hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3(grid), dim3(64), 0, 0, d_desc, nullptr,
                          (uint32_t)B, d_dig);
   };
   launch();
@@ -220,7 +223,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   if (pad) printf("(stride pad %llu) ", (unsigned long long)pad);
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which ? "pc" : "v1", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : "coal", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -268,7 +271,7 @@ static int run_edges(int which) {
   std::vector<std::pair<uint64_t, uint64_t>> ref;
   for (int off = 0; off < 8; ++off)
     for (int i = 0; i < nl; ++i) {
-      uint64_t o = off * 4099 + off;
+      uint64_t o = which == 2 ? off * 4096 + 16 * off : off * 4099 + off;
       desc.push_back({d + o, lens[i]});
       ref.push_back({o, lens[i]});
     }
@@ -282,8 +285,11 @@ static int run_edges(int which) {
   if (which == 0)
     hipLaunchKernelGGL(qsmd5_batch_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, dd, nullptr,
                        (uint32_t)n, dg);
-  else
+  else if (which == 1)
     hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
+                       (uint32_t)n, dg);
+  else
+    hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, dd, nullptr,
                        (uint32_t)n, dg);
   CK(hipDeviceSynchronize());
   std::vector<uint8_t> got(16 * n);
@@ -315,6 +321,56 @@ __global__ __launch_bounds__(256) void k_stream_read(const u32x4* __restrict__ p
     acc ^= v;
   }
   if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1;
+}
+
+// Per-lane sequential streams (the MD5 access pattern with no compute): lane l
+// reads chunk l's bytes 64 B at a time, 8 blocks per iteration in flight.
+template <bool kNT>
+__global__ __launch_bounds__(64) void k_lane_stream(const uint8_t* __restrict__ base,
+                                                    uint64_t stride, uint32_t nblk,
+                                                    uint32_t* sink) {
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  const u32x4* p = reinterpret_cast<const u32x4*>(base + stride * t);
+  u32x4 acc = {0, 0, 0, 0};
+  for (uint32_t j = 0; j < nblk; j += 8) {
+    u32x4 v[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) v[k] = kNT ? __builtin_nontemporal_load(p + 4 * j + k) : p[4 * j + k];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) acc ^= v[k];
+  }
+  if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = t;
+}
+
+static void run_lane_stream(uint32_t B, uint64_t L, uint64_t pad, bool nt) {
+  uint64_t stride = L + pad;
+  uint8_t* d;
+  uint32_t* sink;
+  CK(hipMalloc(&d, stride * B));
+  CK(hipMalloc(&sink, 4));
+  CK(hipMemset(d, 3, stride * B));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float best = 1e30f;
+  for (int r = 0; r < 4; ++r) {
+    CK(hipEventRecord(e0, 0));
+    if (nt)
+      hipLaunchKernelGGL(k_lane_stream<true>, dim3(B / 64), dim3(64), 0, 0, d, stride,
+                         (uint32_t)(L / 64), sink);
+    else
+      hipLaunchKernelGGL(k_lane_stream<false>, dim3(B / 64), dim3(64), 0, 0, d, stride,
+                         (uint32_t)(L / 64), sink);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    if (r) best = ms < best ? ms : best;
+  }
+  printf("lane_stream%s B=%u L=%llu pad=%llu: %.3f ms -> %.1f GB/s\n", nt ? "[nt]" : "", B,
+         (unsigned long long)L, (unsigned long long)pad, best, (double)L * B / (best * 1e-3) / 1e9);
+  CK(hipFree(d));
+  CK(hipFree(sink));
 }
 
 static void run_stream_read(uint64_t bytes, int reps) {
@@ -349,6 +405,28 @@ int main(int argc, char** argv) {
     run_stream_read(4ull << 30, 2);
     run_md5(512, 10485760, 1, false, 1);
     run_md5(131072, 65536, 1, false, 0);
+    return 0;
+  }
+  if (!strcmp(mode, "coal")) {
+    int bad = run_edges(2);
+    for (int w : {0, 2}) {
+      run_md5(131072, 65536, 5, true, w, 0);
+      run_md5(131072, 65536, 5, true, w, 4352);
+      run_md5(262144, 32768, 5, true, w, 4352);
+      run_md5(65536, 262144, 3, true, w, 4352);
+      run_md5(32768, 1 << 20, 3, true, w, 4352);
+    }
+    return bad ? 1 : 0;
+  }
+  if (!strcmp(mode, "mem")) {
+    run_stream_read(8ull << 30, 5);
+    for (int nt = 0; nt < 2; ++nt) {
+      run_lane_stream(131072, 65536, 0, nt);
+      run_lane_stream(131072, 65536, 4352, nt);
+      run_lane_stream(32768, 262144, 4352, nt);
+      run_lane_stream(8192, 1 << 20, 4352, nt);
+      run_lane_stream(512, 10485760, 0, nt);
+    }
     return 0;
   }
   if (!strcmp(mode, "ab")) {
