@@ -469,14 +469,17 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
     src_nblk[i] = (uint32_t)__shfl((int)nblk, c, 64);
     piece[i] = slot ^ (((uint32_t)c >> 1) & 7u);  // 16-B piece this lane fetches
   }
+  // Exactly 8 LDS-DMA instructions per tile, whatever the chain lengths: the
+  // counted vmcnt waits below depend on it.  Lanes whose chain has no whole
+  // block left (or no chain) fetch 16 harmless bytes from the descriptor array.
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(chunks);
   auto issue_tile = [&](uint32_t b, uint32_t tl) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      if (src_nblk[i]) {
-        const uint32_t blk = min(tl * 2u + (piece[i] >> 2), src_nblk[i] - 1u);
-        const uint8_t* g = src[i] + (uint64_t)blk * 64u + (piece[i] & 3u) * 16u;
-        __builtin_amdgcn_global_load_lds(QS_GP(g), QS_LP(&tile_buf[b][i * 8][0]), 16, 0, 0);
-      }
+      const uint32_t blk = min(tl * 2u + (piece[i] >> 2), src_nblk[i] - 1u);
+      const uint8_t* g = src_nblk[i] ? src[i] + (uint64_t)blk * 64u + (piece[i] & 3u) * 16u
+                                     : dummy;
+      __builtin_amdgcn_global_load_lds(QS_GP(g), QS_LP(&tile_buf[b][i * 8][0]), 16, 0, 0);
     }
   };
   const uint32_t rswz = (lane >> 1) & 7u;
