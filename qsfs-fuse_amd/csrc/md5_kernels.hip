@@ -438,12 +438,16 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
 #define QS_GP(p) ((const __attribute__((address_space(1))) void*)(uintptr_t)(p))
 #define QS_LP(p) ((__attribute__((address_space(3))) void*)(uintptr_t)(uint32_t)(uintptr_t)(p))
 
-template <int kBufs>
+template <int kTB, int kBufs>
 __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ chunks,
                                                 const uint32_t* __restrict__ order, uint32_t n,
                                                 uint32_t* __restrict__ digests) {
-  // kBufs tile buffers: kBufs - 1 tiles in flight while one compresses.
-  __shared__ u32x4 tile_buf[kBufs][64][8];
+  // kTB blocks (kTB x 64 B) per chain per tile; kBufs tile buffers: kBufs - 1
+  // tiles in flight while one compresses.  A row of kS 16-B slots per chain;
+  // one LDS-DMA instruction covers 64 / kS chains, kS instructions per tile.
+  constexpr int kS = 4 * kTB;
+  constexpr int kCPI = 64 / kS;  // chains per instruction
+  __shared__ u32x4 tile_buf[kBufs][64][kS];
   const uint32_t lane = threadIdx.x;
   const uint32_t t = blockIdx.x * 64u + lane;
   uint32_t idx = 0;
@@ -453,36 +457,42 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
     cd = chunks[idx];
   }
   const uint32_t nblk = (uint32_t)(cd.len >> 6);
-  const uint32_t ntiles = (wave_max_u32(nblk) + 1u) >> 1;
+  const uint32_t ntiles =
+      __builtin_amdgcn_readfirstlane((wave_max_u32(nblk) + (kTB - 1)) / kTB);
+  // Slot swizzle making the row reads (lane l reads row l) bank-conflict-free
+  // for ds_read_b128's 16-lane groups: rows of 128 B alternate bank halves.
+  auto swz = [](uint32_t c) -> uint32_t {
+    return kTB == 2 ? ((c >> 1) & 7u) : (c & 15u);
+  };
 
-  // Loader role of this lane in instruction i: chain 8i + (lane >> 3), slot lane & 7.
-  const uint32_t slot = lane & 7u;
+  // Loader role of this lane in instruction i: chain kCPI*i + lane / kS, slot lane % kS.
+  const uint32_t slot = lane % kS;
   const uint64_t myptr = reinterpret_cast<uint64_t>(cd.ptr);
-  const uint8_t* src[8];
-  uint32_t src_nblk[8], piece[8];
+  const uint8_t* src[kS];
+  uint32_t src_nblk[kS], piece[kS];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = i * 8 + (int)(lane >> 3);
+  for (int i = 0; i < kS; ++i) {
+    const int c = i * kCPI + (int)(lane / kS);
     const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)myptr, c, 64);
     const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(myptr >> 32), c, 64);
     src[i] = reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo);
     src_nblk[i] = (uint32_t)__shfl((int)nblk, c, 64);
-    piece[i] = slot ^ (((uint32_t)c >> 1) & 7u);  // 16-B piece this lane fetches
+    piece[i] = slot ^ swz((uint32_t)c);  // 16-B piece this lane fetches
   }
-  // Exactly 8 LDS-DMA instructions per tile, whatever the chain lengths: the
+  // Exactly kS LDS-DMA instructions per tile, whatever the chain lengths: the
   // counted vmcnt waits below depend on it.  Lanes whose chain has no whole
   // block left (or no chain) fetch 16 harmless bytes from the descriptor array.
   const uint8_t* dummy = reinterpret_cast<const uint8_t*>(chunks);
   auto issue_tile = [&](uint32_t b, uint32_t tl) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t blk = min(tl * 2u + (piece[i] >> 2), src_nblk[i] - 1u);
+    for (int i = 0; i < kS; ++i) {
+      const uint32_t blk = min(tl * (uint32_t)kTB + (piece[i] >> 2), src_nblk[i] - 1u);
       const uint8_t* g = src_nblk[i] ? src[i] + (uint64_t)blk * 64u + (piece[i] & 3u) * 16u
                                      : dummy;
-      __builtin_amdgcn_global_load_lds(QS_GP(g), QS_LP(&tile_buf[b][i * 8][0]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(QS_GP(g), QS_LP(&tile_buf[b][i * kCPI][0]), 16, 0, 0);
     }
   };
-  const uint32_t rswz = (lane >> 1) & 7u;
+  const uint32_t rswz = swz(lane);
   uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
 #pragma unroll
   for (int k = 0; k < kBufs - 1; ++k)
@@ -491,30 +501,28 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
     const uint32_t b = tl % kBufs;
     if (tl + (kBufs - 1) < ntiles) {
       issue_tile((tl + (kBufs - 1)) % kBufs, tl + (kBufs - 1));
-      // the kBufs - 1 younger tiles (8 LDS-DMA each) may stay in flight
-      if constexpr (kBufs == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      // the kBufs - 1 younger tiles (kS LDS-DMA each) may stay in flight
+      if constexpr (kS * (kBufs - 1) == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if constexpr (kS * (kBufs - 1) == 16) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
-      // tail: fewer tiles follow; drain (rare, last kBufs - 1 tiles only)
+      // last kBufs - 1 tiles: fewer follow, drain
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    u32x4 q[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) q[k] = tile_buf[b][lane][k ^ rswz];
-    uint32_t w[16];
-    if (tl * 2u < nblk) {
-      unpack4(w, 0, q[0]);
-      unpack4(w, 1, q[1]);
-      unpack4(w, 2, q[2]);
-      unpack4(w, 3, q[3]);
-      md5_compress(st, w);
-    }
-    if (tl * 2u + 1u < nblk) {
-      unpack4(w, 0, q[4]);
-      unpack4(w, 1, q[5]);
-      unpack4(w, 2, q[6]);
-      unpack4(w, 3, q[7]);
-      md5_compress(st, w);
+    for (int h = 0; h < kTB; ++h) {
+      u32x4 q0 = tile_buf[b][lane][(4 * h + 0) ^ rswz];
+      u32x4 q1 = tile_buf[b][lane][(4 * h + 1) ^ rswz];
+      u32x4 q2 = tile_buf[b][lane][(4 * h + 2) ^ rswz];
+      u32x4 q3 = tile_buf[b][lane][(4 * h + 3) ^ rswz];
+      if (tl * (uint32_t)kTB + h < nblk) {
+        uint32_t w[16];
+        unpack4(w, 0, q0);
+        unpack4(w, 1, q1);
+        unpack4(w, 2, q2);
+        unpack4(w, 3, q3);
+        md5_compress(st, w);
+      }
     }
     // the next issue_tile may overwrite a buffer: make sure the row reads are done
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -524,13 +532,15 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
   u32x4 o = {st[0], st[1], st[2], st[3]};
   *reinterpret_cast<u32x4*>(digests + 4u * (uint64_t)idx) = o;
 }
-// Two tile buffers (16 KiB LDS per wave, up to 10 waves per CU): a third
-// buffer measured slower at 131072 x 64 KiB (24 KiB per wave cuts residency to
-// 6 waves per CU and the batch no longer fits one round).
+
+// 2-block tiles, two tile buffers (16 KiB LDS per wave, up to 10 waves per
+// CU).  Measured alternatives (profiles/r01_ubench_coal_variants.log): a third
+// buffer, or 4-block tiles (32 KiB per wave), both lose 25-35% at
+// 131072 x 64 KiB -- fewer resident waves, the batch no longer fits one round.
 extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_coal_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
     uint32_t* __restrict__ digests) {
-  batch_coal_body<2>(chunks, order, n, digests);
+  batch_coal_body<2, 2>(chunks, order, n, digests);
 }
 
 #undef QS_GP

@@ -271,7 +271,7 @@ static int run_edges(int which) {
   std::vector<std::pair<uint64_t, uint64_t>> ref;
   for (int off = 0; off < 8; ++off)
     for (int i = 0; i < nl; ++i) {
-      uint64_t o = which == 2 ? off * 4096 + 16 * off : off * 4099 + off;
+      uint64_t o = which >= 2 ? off * 4096 + 16 * off : off * 4099 + off;
       desc.push_back({d + o, lens[i]});
       ref.push_back({o, lens[i]});
     }
