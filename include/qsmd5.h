@@ -160,6 +160,19 @@ QSMD5_API int qsmd5_plan_parts(uint64_t file_size, uint64_t buf_size, uint64_t m
  * at the byte for parts[0].offset (host or device memory). */
 QSMD5_API int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t n, uint8_t (*digests)[16]);
 
+/* Download-side integrity (new: the reference never
+ * hashes downloads).  QSClient::DownloadFile keeps the object's ETag
+ * (QSClient.cpp:321-323) and ReceivedHandlerSingleDownload
+ * (QSTransferManager.cpp:85-98) is where a check belongs.  For a single-part
+ * object the ETag is the MD5 as 32 hex digits, optionally in double quotes.
+ * qsmd5_etag_matches: 1 = digest matches, 0 = mismatch, -EINVAL = the ETag is
+ * not a plain MD5 (multipart "<hex>-<n>", empty, malformed).  Host-only. */
+QSMD5_API int qsmd5_etag_matches(const uint8_t digest[16], const char* etag);
+
+/* Hash [ptr, ptr+len) (host or device memory) and compare with etag:
+ * 1 / 0 as above, or a negative errno. */
+QSMD5_API int qsmd5_verify_etag(const void* ptr, uint64_t len, const char* etag);
+
 /* Timing of the most recent synchronous batch on this process (ms): total
  * wall, and GPU kernel time between the first and last kernel event. */
 QSMD5_API int qsmd5_last_timing(double* wall_ms, double* kernel_ms);

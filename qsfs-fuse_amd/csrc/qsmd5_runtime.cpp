@@ -615,6 +615,38 @@ int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t n, uint8_
   });
 }
 
+int qsmd5_etag_matches(const uint8_t digest[16], const char* etag) {
+  if (!digest || !etag) return fail(-EINVAL, "qsmd5: NULL digest/etag");
+  size_t n = strlen(etag);
+  const char* p = etag;
+  if (n >= 2 && p[0] == '"' && p[n - 1] == '"') {
+    ++p;
+    n -= 2;
+  }
+  if (n != 32) return fail(-EINVAL, "qsmd5: ETag is not a 32-hex-digit MD5");
+  auto nib = [](char c) -> int {
+    if (c >= '0' && c <= '9') return c - '0';
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+    return -1;
+  };
+  int match = 1;
+  for (int i = 0; i < 16; ++i) {
+    const int hi = nib(p[2 * i]), lo = nib(p[2 * i + 1]);
+    if (hi < 0 || lo < 0) return fail(-EINVAL, "qsmd5: ETag is not a 32-hex-digit MD5");
+    if (((hi << 4) | lo) != digest[i]) match = 0;
+  }
+  return match;
+}
+
+int qsmd5_verify_etag(const void* ptr, uint64_t len, const char* etag) {
+  // validate the ETag's form before spending a GPU pass on it
+  uint8_t d[16] = {0};
+  if (int rc = qsmd5_etag_matches(d, etag); rc < 0) return rc;
+  if (int rc = qsmd5_hash_one(ptr, len, d)) return rc;
+  return qsmd5_etag_matches(d, etag);
+}
+
 int qsmd5_last_timing(double* wall_ms, double* kernel_ms) {
   Runtime& r = rt();
   std::lock_guard<std::mutex> lk(r.mu);

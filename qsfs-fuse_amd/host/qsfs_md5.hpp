@@ -116,6 +116,15 @@ std::string md5(const StreamPtr& stream) {
   return out;
 }
 
+// Download-side integrity check: true if the MD5 of
+// [p, p+len) equals a single-part object's ETag (QSClient.cpp:321-323).
+// Throws qsmd5::Error for a multipart/malformed ETag or a GPU failure.
+inline bool verify_etag(const void* p, uint64_t len, const std::string& etag) {
+  const int rc = qsmd5_verify_etag(p, len, etag.c_str());
+  if (rc < 0) throw Error(rc, "qsmd5_verify_etag");
+  return rc == 1;
+}
+
 // class MD5 -- MD5.h:51-93, over the streaming C-ABI context.
 class MD5 {
  public:

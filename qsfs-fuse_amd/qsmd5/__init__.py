@@ -19,7 +19,8 @@ import os
 __all__ = [
     "Md5Error", "lib", "lib_path", "hexdigest", "md5", "md5_stream", "MD5", "hash_batch",
     "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
-    "alloc_pinned", "free_pinned", "synth_fill_lcg", "last_timing", "Part",
+    "alloc_pinned", "free_pinned", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
+    "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -102,6 +103,8 @@ def lib():
             ctypes.POINTER(Part), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
         "qsmd5_hash_parts": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Part), ctypes.c_size_t,
                                             c_u8p]),
+        "qsmd5_etag_matches": (ctypes.c_int, [c_u8p, ctypes.c_char_p]),
+        "qsmd5_verify_etag": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p]),
         "qsmd5_last_timing": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]),
         "qsmd5_synth_fill_lcg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
@@ -304,6 +307,26 @@ class MD5(object):
                 self._ctx = ctypes.c_void_p()
         except Exception:
             pass
+
+
+def etag_matches(digest, etag):
+    """qsmd5_etag_matches: True/False, or raises Md5Error(-EINVAL) for a
+    multipart / malformed ETag."""
+    d = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(digest))
+    rc = lib().qsmd5_etag_matches(d, etag.encode() if isinstance(etag, str) else etag)
+    if rc < 0:
+        raise Md5Error(rc, "qsmd5_etag_matches")
+    return rc == 1
+
+
+def verify_etag(buf, etag):
+    """Hash a downloaded buffer (host or device) on the GPU and compare with its ETag."""
+    keep = []
+    p, L = _as_chunk(buf, keep)
+    rc = lib().qsmd5_verify_etag(p, L, etag.encode() if isinstance(etag, str) else etag)
+    if rc < 0:
+        raise Md5Error(rc, "qsmd5_verify_etag")
+    return rc == 1
 
 
 def alloc_pinned(nbytes):

@@ -146,3 +146,18 @@ def test_no_gpu_fails_loudly():
         qsmd5.hash_batch([b"abc", b"def"])
     with pytest.raises(qsmd5.Md5Error):
         qsmd5.MD5("abc")
+
+
+def test_etag_matching_rules():
+    """Single-part ETag = the MD5 hex, optionally quoted; multipart ETags are refused."""
+    import hashlib
+    d = hashlib.md5(b"qsfs").digest()
+    h = d.hex()
+    assert qsmd5.etag_matches(d, h)
+    assert qsmd5.etag_matches(d, '"%s"' % h)
+    assert qsmd5.etag_matches(d, h.upper())
+    assert not qsmd5.etag_matches(d, "0" * 32)
+    for bad in ["", '""', h[:31], h + "0", '"%s-3"' % h, "g" * 32, "%s-12" % h[:29]]:
+        with pytest.raises(qsmd5.Md5Error) as e:
+            qsmd5.etag_matches(d, bad)
+        assert e.value.code == -errno.EINVAL

@@ -312,3 +312,15 @@ def test_coalesced_kernel_device_async_large():
     want = md5_many([(host.ctypes.data + i * S, L) for i in sample])
     got = [bytes(dig[i].cpu().numpy()) for i in sample]
     assert got == want
+
+
+def test_verify_etag_download_buffer():
+    import hashlib
+    data = bytes(lcg_bytes(55, 3 * MiB + 17))
+    etag = '"%s"' % hashlib.md5(data).hexdigest()
+    assert qsmd5.verify_etag(data, etag)
+    dev = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
+    assert qsmd5.verify_etag(dev, etag)
+    assert not qsmd5.verify_etag(data[:-1], etag)
+    with pytest.raises(qsmd5.Md5Error):
+        qsmd5.verify_etag(data, etag[:-2] + '-2"')

@@ -1,0 +1,100 @@
+"""Process-level behaviour of the GPU path on an MI355X.
+
+- init after fork: qsfs daemonises inside fuse_main() and starts its threads in
+  qsfs_init afterwards (Operations.cpp:1520-1549, Mounter.cpp:90-95); the
+  library initialises lazily, so a child forked before any GPU use hashes
+  correctly, and so does the parent afterwards;
+- several processes hashing on one GPU at once (qsfs instances per mount);
+- the N>1 bench flow (sharding, digest gather, max-over-ranks timing, one
+  JSON line) rehearsed with 2 ranks on the one GPU over gloo.
+Each case runs in child processes, never in the (GPU-initialised) pytest
+process itself.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+PY = sys.executable
+ENV = dict(os.environ, PYTHONPATH=os.pathsep.join(
+    [os.path.join(ROOT, "qsfs-fuse_amd"), os.path.join(ROOT, "tests")]))
+
+FORK_SCRIPT = r'''
+import os, sys
+import qsmd5
+L = qsmd5.lib()          # library loaded, no HIP call yet
+pid = os.fork()
+if pid == 0:             # the daemon side of fuse_main's fork
+    try:
+        ok = qsmd5.md5("abc") == "900150983cd24fb0d6963f7d28e17f72"
+        ok = ok and qsmd5.hash_batch([b"x" * 1000, b""])[1].hex() == "d41d8cd98f00b204e9800998ecf8427e"
+    except Exception as e:
+        print("child error", e, file=sys.stderr)
+        ok = False
+    os._exit(0 if ok else 3)
+_, st = os.waitpid(pid, 0)
+child_ok = os.WIFEXITED(st) and os.WEXITSTATUS(st) == 0
+parent_ok = qsmd5.md5("message digest") == "f96b697d7cb7938d525a2f31aaf161d0"
+print("child_ok=%s parent_ok=%s" % (child_ok, parent_ok))
+sys.exit(0 if child_ok and parent_ok else 1)
+'''
+
+WORKER_SCRIPT = r'''
+import sys, ctypes
+import qsmd5
+from oracle_util import lcg_bytes, md5_many
+seed = int(sys.argv[1])
+bufs = [lcg_bytes(seed * 100 + i, (1 << 20) + 37 * i) for i in range(24)]
+want = md5_many([(b, (1 << 20) + 37 * i) for i, b in enumerate(bufs)])
+for _ in range(3):
+    got = qsmd5.hash_batch([(ctypes.addressof(b), (1 << 20) + 37 * i) for i, b in enumerate(bufs)])
+    if got != want:
+        sys.exit(2)
+print("worker", seed, "ok")
+'''
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_init_after_fork():
+    out = subprocess.run([PY, "-c", FORK_SCRIPT], env=ENV, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "child_ok=True parent_ok=True" in out.stdout
+
+
+def test_concurrent_processes_one_gpu():
+    procs = [subprocess.Popen([PY, "-c", WORKER_SCRIPT, str(k)], env=ENV,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for k in range(3)]
+    for p in procs:
+        o, e = p.communicate(timeout=300)
+        assert p.returncode == 0, o + e
+
+
+def test_bench_two_rank_rehearsal():
+    cmd = [PY, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "64", "--rehearse-gloo"]
+    out = subprocess.run(cmd, env=ENV, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 128
+    assert r["parity"].startswith("ok: 128/128")
+    assert r["cpu_baseline"] is None and r["scaling"] == "weak"
