@@ -1,0 +1,54 @@
+"""qsmd5sum: the batch caller end to end on the GPU.
+
+Files are sliced like QSTransferManager::PrepareUpload, gathered into pinned
+buffers and hashed in one qsmd5_hash_batch call; every printed digest is
+checked against hashlib on the same byte range.
+"""
+import hashlib
+import os
+import subprocess
+import tempfile
+
+import pytest
+
+import qsmd5
+from conftest import ROOT
+from oracle_util import lcg_bytes
+
+pytestmark = pytest.mark.gpu
+MiB = 1 << 20
+TOOL = os.path.join(ROOT, "qsfs-fuse_amd", "bin", "qsmd5sum")
+
+
+def test_qsmd5sum_parts_match_hashlib():
+    if not os.path.exists(TOOL):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "qsfs-fuse_amd")])
+    sizes = [0, 5, 19 * MiB, 20 * MiB, 21 * MiB + 3, 25 * MiB, 64 * MiB + 1]
+    with tempfile.TemporaryDirectory() as td:
+        paths, blobs = [], []
+        for i, sz in enumerate(sizes):
+            b = bytes(lcg_bytes(500 + i, sz))[:sz]
+            p = os.path.join(td, "f%d" % i)
+            with open(p, "wb") as f:
+                f.write(b)
+            paths.append(p)
+            blobs.append(b)
+        out = subprocess.run([TOOL] + paths, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr
+        lines = out.stdout.strip().splitlines()
+        want = []
+        for p, b in zip(paths, blobs):
+            parts = qsmd5.plan_parts(len(b))
+            if len(parts) == 1 and len(b) < 20 * MiB:
+                want.append("%s  %s" % (hashlib.md5(b).hexdigest(), p))
+            else:
+                for q in parts:
+                    want.append("%s  %s#%d %d %d" % (
+                        hashlib.md5(b[q.offset:q.offset + q.size]).hexdigest(), p,
+                        q.part_number, q.offset, q.size))
+        assert lines == want
+        # -b 1: 1 MiB parts (the -b option of qsfs, Parser.cpp:167)
+        out = subprocess.run([TOOL, "-b", "1", "--parts", paths[5]], capture_output=True,
+                             text=True, timeout=300)
+        assert out.returncode == 0, out.stderr
+        assert len(out.stdout.strip().splitlines()) == 25
