@@ -132,6 +132,9 @@ def main():
     ap.add_argument("--batch", type=int, default=BATCH, help="chunks per GPU (default 512)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--dist-always", action="store_true",
+                    help="init the process group and gather digests even at world size 1 "
+                         "(exercises the RCCL path on a 1-GPU box)")
     ap.add_argument("--rehearse-gloo", action="store_true",
                     help="N>1 rehearsal on a 1-GPU box: every rank on cuda:0, gloo digest gather")
     args = ap.parse_args()
@@ -152,8 +155,10 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    distributed = world > 1 or args.dist_always
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
         if args.rehearse_gloo:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
@@ -184,7 +189,7 @@ def main():
         qsmd5.hash_device(desc.data_ptr(), dig.data_ptr(), B, stream=sp)
         if ev is not None:
             ev[1].record(stream)
-        if world > 1:
+        if distributed:
             return gather_digests(dig, B * world)
         return dig
 
@@ -193,7 +198,7 @@ def main():
     torch.cuda.synchronize()
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -201,11 +206,11 @@ def main():
     for k in range(args.steps):
         out = step(events[k])
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    if world > 1:
+    if distributed:
         tt = torch.tensor([elapsed], dtype=torch.float64,
                           device="cpu" if args.rehearse_gloo else dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -268,7 +273,7 @@ def main():
         del host
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
     return 0 if parity_ok else 3
 
