@@ -81,7 +81,7 @@ def config1():
                   "CPU core here; batches are what the GPU path is for"})
 
 
-def config3(reps, n=4096):
+def config3(reps, n=4096, label=""):
     import numpy as np
     import torch
     import qsmd5
@@ -104,7 +104,7 @@ def config3(reps, n=4096):
         wall, kern = qsmd5.last_timing()
         ok = [d.hex() for d in digs] == g
         emit({"config": 3, "workload": "%d x 10 MiB in pinned host memory, end-to-end "
-                                       "(H2D + hash + D2H digests)" % n,
+                                       "(H2D + hash + D2H digests)%s" % (n, label),
               "value": round(n * L / GiB / dt, 3), "unit": "GiB/s", "seconds": round(dt, 4),
               "last_call_wall_ms": round(wall, 2), "last_call_kernel_window_ms": round(kern, 2),
               "parity": "ok: %d/%d == reference golden" % (n, n) if ok else "FAIL"})

@@ -42,6 +42,7 @@ using qsmd5::kKernelThroughput;
 
 constexpr uint64_t kMaxChunkLen = 1ull << 38;
 constexpr int kComputeStreams = 8;
+constexpr int kMaxCopyStreams = 4;
 constexpr uint64_t kSliceMin = 512ull << 20;        // H2D slice bounds
 constexpr uint64_t kSliceMax = 4ull << 30;
 constexpr uint64_t kDefaultStaging = 16ull << 30;   // device staging ring
@@ -118,12 +119,30 @@ struct HostPinned {
   }
 };
 
+// Events of one batch, destroyed together when the batch returns.
+struct EventSet {
+  std::vector<hipEvent_t> ev;
+  EventSet() = default;
+  EventSet(const EventSet&) = delete;
+  EventSet& operator=(const EventSet&) = delete;
+  ~EventSet() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+  int make(hipEvent_t* out, unsigned flags) {
+    hipError_t e = hipEventCreateWithFlags(out, flags);
+    if (e != hipSuccess) return hip_fail(e, "hipEventCreate");
+    ev.push_back(*out);
+    return 0;
+  }
+};
+
 struct Runtime {
   std::mutex mu;  // serialises batches on the device
   bool ready = false;
   int init_rc = 0;
   int device = -1;
-  hipStream_t copy = nullptr;
+  hipStream_t copy[kMaxCopyStreams] = {};
+  int ncopy = 2;  // H2D streams (QSMD5_COPY_STREAMS), slices alternate over them
   hipStream_t compute[kComputeStreams] = {};
   DevBuf d_desc, d_order, d_dig, d_staging;
   HostPinned h_desc, h_order, h_dig;
@@ -158,9 +177,13 @@ void do_init() {
     r.init_rc = hip_fail(e, "hipSetDevice");
     return;
   }
-  if ((e = hipStreamCreateWithFlags(&r.copy, hipStreamNonBlocking)) != hipSuccess) {
-    r.init_rc = hip_fail(e, "hipStreamCreate");
-    return;
+  r.ncopy = (int)std::min<uint64_t>(kMaxCopyStreams,
+                                     std::max<uint64_t>(1, env_u64("QSMD5_COPY_STREAMS", 2)));
+  for (int k = 0; k < r.ncopy; ++k) {
+    if ((e = hipStreamCreateWithFlags(&r.copy[k], hipStreamNonBlocking)) != hipSuccess) {
+      r.init_rc = hip_fail(e, "hipStreamCreate");
+      return;
+    }
   }
   for (auto& s : r.compute) {
     if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) {
@@ -285,14 +308,12 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   uint32_t* ho = static_cast<uint32_t*>(r.h_order.p);
   for (size_t i = 0; i < n; ++i) hd[i] = {len[i] ? chunks[i].ptr : nullptr, len[i]};
   uint8_t* stage = static_cast<uint8_t*>(r.d_staging.p);
-  std::vector<std::vector<uint64_t>> stage_off(slices.size());
   for (size_t si = 0; si < slices.size(); ++si) {
     uint8_t* base = stage + (si % nregions) * region;
     uint64_t off = 0;
     for (size_t k = 0; k < slices[si].count; ++k) {
       uint32_t ci = host_idx[slices[si].first + k];
       hd[ci].ptr = base + off;
-      stage_off[si].push_back(off);
       off += stage_bytes(len[ci]);
     }
   }
@@ -301,20 +322,22 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   for (uint32_t ci : host_idx) ho[pos++] = ci;
 
   hipStream_t s0 = r.compute[0];
+  EventSet events;
+  // On any failure after work was enqueued, wait for it before returning: an
+  // H2D copy may still be reading the caller's buffers.
+  auto drain = [&](int code) {
+    for (int k = 0; k < r.ncopy; ++k) (void)hipStreamSynchronize(r.copy[k]);
+    for (hipStream_t s : r.compute) (void)hipStreamSynchronize(s);
+    return code;
+  };
   QS_HIP(hipMemcpyAsync(r.d_desc.p, hd, n * sizeof(qsmd5_chunk), hipMemcpyHostToDevice, s0));
   QS_HIP(hipMemcpyAsync(r.d_order.p, ho, n * sizeof(uint32_t), hipMemcpyHostToDevice, s0));
-  hipEvent_t meta_ready, k_first = nullptr, k_last = nullptr;
-  QS_HIP(hipEventCreateWithFlags(&meta_ready, hipEventDisableTiming));
+  hipEvent_t meta_ready = nullptr, k_first = nullptr, k_last = nullptr;
+  if (int rc = events.make(&meta_ready, hipEventDisableTiming)) return drain(rc);
+  if (int rc = events.make(&k_first, hipEventDefault)) return drain(rc);
+  if (int rc = events.make(&k_last, hipEventDefault)) return drain(rc);
   QS_HIP(hipEventRecord(meta_ready, s0));
-  QS_HIP(hipEventCreate(&k_first));
-  QS_HIP(hipEventCreate(&k_last));
   std::vector<hipEvent_t> region_free(nregions, nullptr);
-  std::vector<hipEvent_t> to_destroy;
-  int rc = 0;
-  auto cleanup = [&]() {
-    (void)hipEventDestroy(meta_ready);
-    for (hipEvent_t e : to_destroy) (void)hipEventDestroy(e);
-  };
   const uint32_t* d_order = static_cast<const uint32_t*>(r.d_order.p);
   uint32_t* d_dig = static_cast<uint32_t*>(r.d_dig.p);
   bool first_kernel = true;
@@ -334,95 +357,58 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
     bool aligned16 = true;
     for (uint32_t ci : dev_idx)
       aligned16 = aligned16 && (reinterpret_cast<uintptr_t>(hd[ci].ptr) & 15u) == 0;
-    if ((rc = launch(s0, d_order, dev_idx.size(), aligned16))) {
-      cleanup();
-      return rc;
-    }
+    if (int rc = launch(s0, d_order, dev_idx.size(), aligned16)) return drain(rc);
   }
-  // Host-resident slices.
-  for (size_t si = 0; si < slices.size() && rc == 0; ++si) {
+  // Host-resident slices: H2D on the copy stream into the slice's ring region
+  // (after the kernel that last used the region), then a launch on its own
+  // compute stream once the copy and the descriptors have landed.
+  for (size_t si = 0; si < slices.size(); ++si) {
     const size_t reg = si % nregions;
     hipStream_t cs = r.compute[1 + si % (kComputeStreams - 1)];
+    hipStream_t cp = r.copy[si % r.ncopy];
     if (region_free[reg]) {
-      hipError_t e = hipStreamWaitEvent(r.copy, region_free[reg], 0);
-      if (e != hipSuccess) rc = hip_fail(e, "hipStreamWaitEvent");
+      hipError_t e = hipStreamWaitEvent(cp, region_free[reg], 0);
+      if (e != hipSuccess) return drain(hip_fail(e, "hipStreamWaitEvent"));
     }
-    for (size_t k = 0; k < slices[si].count && rc == 0; ++k) {
+    for (size_t k = 0; k < slices[si].count; ++k) {
       uint32_t ci = host_idx[slices[si].first + k];
       if (len[ci] == 0) continue;
       hipError_t e = hipMemcpyAsync(const_cast<void*>(hd[ci].ptr), chunks[ci].ptr, len[ci],
-                                    hipMemcpyHostToDevice, r.copy);
-      if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync H2D");
+                                    hipMemcpyHostToDevice, cp);
+      if (e != hipSuccess) return drain(hip_fail(e, "hipMemcpyAsync H2D"));
     }
-    if (rc) break;
-    hipEvent_t copied;
-    if (hipEventCreateWithFlags(&copied, hipEventDisableTiming) != hipSuccess ||
-        hipEventRecord(copied, r.copy) != hipSuccess) {
-      rc = fail(-EIO, "qsmd5: event record failed");
-      break;
-    }
-    to_destroy.push_back(copied);
-    if (hipStreamWaitEvent(cs, copied, 0) != hipSuccess ||
-        hipStreamWaitEvent(cs, meta_ready, 0) != hipSuccess) {
-      rc = fail(-EIO, "qsmd5: stream wait failed");
-      break;
-    }
+    hipEvent_t copied = nullptr, done = nullptr;
+    if (int rc = events.make(&copied, hipEventDisableTiming)) return drain(rc);
+    if (int rc = events.make(&done, hipEventDisableTiming)) return drain(rc);
+    hipError_t e = hipEventRecord(copied, cp);
+    if (e == hipSuccess) e = hipStreamWaitEvent(cs, copied, 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(cs, meta_ready, 0);
+    if (e != hipSuccess) return drain(hip_fail(e, "stream ordering"));
     // staged chunks sit at 256-B-aligned offsets plus a 16-B-multiple skew
-    if ((rc = launch(cs, d_order + dev_idx.size() + slices[si].first, slices[si].count, true)))
-      break;
-    hipEvent_t done;
-    if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess ||
-        hipEventRecord(done, cs) != hipSuccess) {
-      rc = fail(-EIO, "qsmd5: event record failed");
-      break;
-    }
-    to_destroy.push_back(done);
+    if (int rc = launch(cs, d_order + dev_idx.size() + slices[si].first, slices[si].count, true))
+      return drain(rc);
+    if ((e = hipEventRecord(done, cs)) != hipSuccess) return drain(hip_fail(e, "hipEventRecord"));
     region_free[reg] = done;
   }
-  if (rc) {
-    (void)hipDeviceSynchronize();
-    cleanup();
-    return rc;
-  }
-  // Join every compute stream into s0, then fetch digests.
+  // Join every compute stream into s0, then fetch the digests.
   for (int k = 1; k < kComputeStreams; ++k) {
-    hipEvent_t j;
-    if (hipEventCreateWithFlags(&j, hipEventDisableTiming) != hipSuccess) {
-      rc = fail(-EIO, "qsmd5: event create failed");
-      break;
-    }
-    to_destroy.push_back(j);
-    if (hipEventRecord(j, r.compute[k]) != hipSuccess || hipStreamWaitEvent(s0, j, 0) != hipSuccess) {
-      rc = fail(-EIO, "qsmd5: stream join failed");
-      break;
-    }
+    hipEvent_t j = nullptr;
+    if (int rc = events.make(&j, hipEventDisableTiming)) return drain(rc);
+    hipError_t e = hipEventRecord(j, r.compute[k]);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s0, j, 0);
+    if (e != hipSuccess) return drain(hip_fail(e, "stream join"));
   }
-  if (rc == 0 && !first_kernel) {
-    hipError_t e = hipEventRecord(k_last, s0);
-    if (e != hipSuccess) rc = hip_fail(e, "hipEventRecord");
-  }
-  if (rc == 0) {
-    hipError_t e = hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0);
-    if (e != hipSuccess) rc = hip_fail(e, "hipMemcpyAsync D2H");
-  }
-  if (rc == 0) {
-    hipError_t e = hipStreamSynchronize(s0);
-    if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
-  }
-  if (rc == 0) {
-    memcpy(digests, r.h_dig.p, n * 16);
-    float kms = 0;
-    if (!first_kernel && hipEventElapsedTime(&kms, k_first, k_last) == hipSuccess)
-      r.last_kernel_ms = kms;
-    else
-      r.last_kernel_ms = 0;
-    r.last_wall_ms =
-        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  }
-  (void)hipEventDestroy(k_first);
-  (void)hipEventDestroy(k_last);
-  cleanup();
-  return rc;
+  if (!first_kernel) QS_HIP(hipEventRecord(k_last, s0));
+  QS_HIP(hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0));
+  hipError_t e = hipStreamSynchronize(s0);
+  if (e != hipSuccess) return drain(hip_fail(e, "hipStreamSynchronize"));
+  memcpy(digests, r.h_dig.p, n * 16);
+  float kms = 0;
+  r.last_kernel_ms =
+      (!first_kernel && hipEventElapsedTime(&kms, k_first, k_last) == hipSuccess) ? kms : 0.0;
+  r.last_wall_ms =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return 0;
 }
 
 template <class F>
