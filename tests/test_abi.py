@@ -161,3 +161,14 @@ def test_etag_matching_rules():
         with pytest.raises(qsmd5.Md5Error) as e:
             qsmd5.etag_matches(d, bad)
         assert e.value.code == -errno.EINVAL
+
+
+BOOST = "/root/reference/third_party/boost_1_49_0"
+
+
+@pytest.mark.skipif(not os.path.isdir(BOOST), reason="reference boost headers not present")
+def test_dropin_compiles_with_boost_shared_ptr(tmp_path):
+    """qsfs passes boost::shared_ptr<std::iostream>; the drop-in template must take it."""
+    src = os.path.join(ROOT, "tests", "cpp", "compile_boost_shim.cpp")
+    subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-w",
+                           "-I" + BOOST, src])
