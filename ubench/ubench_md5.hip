@@ -170,10 +170,15 @@ static double run_issue(ukern k, int instr_per_iter, int iters, int threads) {
 }
 
 // ---- 2. MD5 batch kernel -----------------------------------------------------
+static bool g_host_pinned = false;  // "zc" mode: chunks in pinned host memory (zero-copy)
+
 static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint64_t pad = 0) {
   uint64_t stride = ((L + 255) & ~uint64_t(255)) + pad;
   uint8_t* d_data;
-  CK(hipMalloc(&d_data, stride * (uint64_t)B));
+  if (g_host_pinned)
+    CK(hipHostMalloc(&d_data, stride * (uint64_t)B, hipHostMallocDefault));
+  else
+    CK(hipMalloc(&d_data, stride * (uint64_t)B));
   const uint64_t segs = (L + 1023) / 1024;
   const uint64_t thr = segs * (uint64_t)B;
   hipLaunchKernelGGL(qsmd5_lcg_fill_kernel, dim3((thr + 255) / 256), dim3(256), 0, 0, d_data,
@@ -221,6 +226,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   med = s[s.size() / 2];
   double gib = (double)L * B / (1u << 30);
   if (pad) printf("(stride pad %llu) ", (unsigned long long)pad);
+  if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
          which == 0 ? "v1" : which == 1 ? "pc" : "coal", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
@@ -252,7 +258,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     }
     printf("  check %d chunks: %s\n", ncheck, bad ? "FAIL" : "ok");
   }
-  CK(hipFree(d_data));
+  if (g_host_pinned) CK(hipHostFree(d_data)); else CK(hipFree(d_data));
   CK(hipFree(d_desc));
   CK(hipFree(d_dig));
 }
@@ -405,6 +411,16 @@ int main(int argc, char** argv) {
     run_stream_read(4ull << 30, 2);
     run_md5(512, 10485760, 1, false, 1);
     run_md5(131072, 65536, 1, false, 0);
+    return 0;
+  }
+  if (!strcmp(mode, "zc")) {
+    g_host_pinned = true;
+    run_md5(64, 10485760, 2, true, 1);
+    run_md5(512, 10485760, 2, true, 1);
+    run_md5(512, 10485760, 2, true, 0);
+    run_md5(2048, 10485760, 2, true, 1);
+    run_md5(4096, 10485760, 2, true, 1);
+    run_md5(4096, 10485760, 2, true, 0);
     return 0;
   }
   if (!strcmp(mode, "coal")) {
