@@ -1,22 +1,30 @@
 // qsfs-fuse_amd/csrc/md5_kernels.hip -- gfx950 kernels for the qsfs MD5 path.
 //
-// Kernels
-//   qsmd5_batch_kernel   one lane per chunk (qsfs upload part); hashes the
-//                        whole message incl. RFC 1321 padding and writes the
-//                        16-byte digest.  Replaces md5(shared_ptr<iostream>)
-//                        (reference src/base/MD5.cpp:341-349) for a batch.
-//   qsmd5_blocks_kernel  advances one streaming state over whole blocks
-//                        (the MD5 class's update(), MD5.cpp:240-269).
-//   qsmd5_lcg_fill_kernel synthetic-data generator (bench/tests only): the
-//                        LCG of SURVEY.md §8c, jump-ahead parallel.
+// Batch kernels (one lane per chunk = one qsfs upload part; each hashes the
+// whole message incl. RFC 1321 padding and writes the 16-byte digest, i.e.
+// md5(shared_ptr<iostream>), reference src/base/MD5.cpp:341-349, for a batch):
+//   qsmd5_batch_pc_kernel    latency kernel, <= 256 x 64 chunks (every
+//                            BASELINE config): producer wave streams blocks and
+//                            precomputes x[g]+K into LDS, chain wave runs only
+//                            the serial 4-VALU steps.
+//   qsmd5_batch_coal_kernel  throughput kernel, more chunks, 16-B aligned:
+//                            coalesced LDS-DMA staging of 128 B per chain.
+//   qsmd5_batch_kernel       throughput kernel, more chunks, any alignment:
+//                            per-lane loads, 5 VALU per step.
+// Streaming kernels (the MD5 class, MD5.cpp:240-312):
+//   qsmd5_blocks_kernel      advances one state over whole blocks (update()).
+//   qsmd5_final_kernel       tail + padding + length (finalize()).
+// Test/bench support:
+//   qsmd5_lcg_fill_kernel    SURVEY.md §8c LCG data, jump-ahead parallel.
 //
 // Why lane-per-chunk: MD5 is Merkle-Damgard, so a chunk is a strictly serial
-// chain of 64-byte compressions; parallelism exists only across chunks.  A
-// wave issues one instruction per ~4 cycles when alone on its SIMD, so the
-// per-chain rate is set by instructions per block, not by lanes per wave --
-// packing 64 chains into one wave costs nothing per chain and leaves the other
-// SIMDs free.  Workgroups are one wave each so the dispatcher spreads them
-// over all 8 XCDs / 256 CUs.
+// chain of 64-byte compressions; parallelism exists only across chunks.  On
+// gfx950 one wave issues a dependent VALU op every ~4.4 cycles whether 1 or 64
+// lanes are active (ubench/ubench_md5.hip "issue"), so the per-chain rate is
+// set by the dependent instructions per block (4 per step, 256 per block at
+// best), not by lanes per wave: 64 chains share one wave at no cost per chain
+// and leave the other SIMDs free.  Batch workgroups each own 64 chunks, so the
+// dispatcher spreads them over all 8 XCDs / 256 CUs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -458,6 +458,13 @@ int main(int argc, char** argv) {
   if (!strcmp(mode, "issue")) {
     const int iters = 20000;
     printf("  dep v_add_u32      %.2f\n", run_issue(k_dep_add, 64, iters, 64));
+    printf("  dep v_add_u32 32 lanes  %.2f\n", run_issue(k_dep_add, 64, iters, 32));
+    printf("  dep v_add_u32 16 lanes  %.2f\n", run_issue(k_dep_add, 64, iters, 16));
+    printf("  dep v_add_u32 1 lane    %.2f\n", run_issue(k_dep_add, 64, iters, 1));
+    printf("  ind v_add_u32 x4 32 lanes %.2f\n", run_issue(k_ind_add, 256, iters, 32));
+    printf("  md5 step4 64 lanes %.2f per instr\n", run_issue(k_md5_step4, 256, iters, 64));
+    printf("  md5 step4 32 lanes %.2f per instr\n", run_issue(k_md5_step4, 256, iters, 32));
+    printf("  md5 step4 1 lane   %.2f per instr\n", run_issue(k_md5_step4, 256, iters, 1));
     printf("  4 v_add + ds_read  %.2f per group\n", run_issue(k_mix_lds, 64, iters, 64));
     return 0;
   }
