@@ -131,6 +131,15 @@ QSMD5_API int qsmd5_kernel_choice_ex(size_t n, int flags);
  * out must hold 33 bytes (NUL-terminated).  Host-only, needs no GPU. */
 QSMD5_API void qsmd5_hex(const uint8_t digest[16], char out[33]);
 
+/* RFC 1864 Content-MD5 header value: standard base64 (RFC 4648 §4, '='
+ * padded) of the 16 raw digest bytes, 24 chars; out must hold 25 bytes.
+ * The reference hands the SDK the hex text (QSClient.cpp:370, 446) and how
+ * qingstor-sdk-cpp (unpinned, GIT_TAG master) puts it on the wire is not
+ * covered by any reference test: this is the form S3-style
+ * servers verify, offered for callers that set the header themselves.
+ * Host-only, needs no GPU. */
+QSMD5_API void qsmd5_base64(const uint8_t digest[16], char out[25]);
+
 /* Streaming context: the reference MD5 class (update()* then finalize()). */
 typedef struct qsmd5_ctx qsmd5_ctx;
 QSMD5_API int qsmd5_ctx_create(qsmd5_ctx** out);

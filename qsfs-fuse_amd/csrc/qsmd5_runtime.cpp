@@ -480,6 +480,24 @@ void qsmd5_hex(const uint8_t digest[16], char out[33]) {
   out[32] = 0;
 }
 
+void qsmd5_base64(const uint8_t digest[16], char out[25]) {
+  static const char kB64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+  char* o = out;
+  for (int i = 0; i < 15; i += 3) {  // 5 full groups of 3 bytes
+    const uint32_t v = (uint32_t)digest[i] << 16 | (uint32_t)digest[i + 1] << 8 | digest[i + 2];
+    *o++ = kB64[v >> 18];
+    *o++ = kB64[(v >> 12) & 63];
+    *o++ = kB64[(v >> 6) & 63];
+    *o++ = kB64[v & 63];
+  }
+  const uint32_t last = digest[15];  // 1 trailing byte -> 2 chars + "=="
+  *o++ = kB64[last >> 2];
+  *o++ = kB64[(last & 3) << 4];
+  *o++ = '=';
+  *o++ = '=';
+  *o = 0;
+}
+
 int qsmd5_hash_batch_ex(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
   return guarded([&] {
     if (n == 0) return 0;

@@ -125,6 +125,23 @@ inline bool verify_etag(const void* p, uint64_t len, const std::string& etag) {
   return rc == 1;
 }
 
+// RFC 1864 Content-MD5 header value (base64 of the raw digest) from the
+// 32-char hex text md5() returns.  Throws on bad hex.
+inline std::string content_md5_from_hex(const std::string& hex) {
+  if (hex.size() != 32) throw Error(-22, "content_md5_from_hex: need 32 hex chars");
+  uint8_t d[16];
+  for (int i = 0; i < 32; ++i) {
+    const char c = hex[i];
+    const int v = c >= '0' && c <= '9' ? c - '0' : c >= 'a' && c <= 'f' ? c - 'a' + 10
+                : c >= 'A' && c <= 'F' ? c - 'A' + 10 : -1;
+    if (v < 0) throw Error(-22, "content_md5_from_hex: not hex");
+    d[i / 2] = (uint8_t)(i % 2 ? (d[i / 2] | v) : v << 4);
+  }
+  char b[25];
+  qsmd5_base64(d, b);
+  return std::string(b, 24);
+}
+
 // class MD5 -- MD5.h:51-93, over the streaming C-ABI context.
 class MD5 {
  public:

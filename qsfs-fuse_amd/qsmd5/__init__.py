@@ -93,6 +93,7 @@ def lib():
                                                             ctypes.c_size_t, ctypes.c_void_p,
                                                             ctypes.c_void_p, ctypes.c_int]),
         "qsmd5_hex": (None, [c_u8p, ctypes.c_char_p]),
+        "qsmd5_base64": (None, [c_u8p, ctypes.c_char_p]),
         "qsmd5_ctx_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p)]),
         "qsmd5_ctx_update": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
         "qsmd5_ctx_final": (ctypes.c_int, [ctypes.c_void_p, c_u8p]),
@@ -149,6 +150,14 @@ def hexdigest(digest):
     d = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(digest))
     out = ctypes.create_string_buffer(33)
     lib().qsmd5_hex(d, out)
+    return out.value.decode()
+
+
+def content_md5(digest):
+    """16 raw bytes -> RFC 1864 Content-MD5 header value (base64, 24 chars)."""
+    d = (ctypes.c_uint8 * 16).from_buffer_copy(bytes(digest))
+    out = ctypes.create_string_buffer(25)
+    lib().qsmd5_base64(d, out)
     return out.value.decode()
 
 

@@ -80,6 +80,7 @@ int main() {
   std::printf("str_empty %s\n", md5(std::string()).c_str());
   std::printf("str_abc %s\n", md5(std::string("abc")).c_str());
   std::printf("str_literal %s\n", md5("message digest").c_str());
+  std::printf("content_md5_abc %s\n", qsmd5::content_md5_from_hex(md5(std::string("abc"))).c_str());
 
   // 2. md5(shared_ptr<iostream>) over a StreamBuf-style view (lengthToRead < size).
   for (size_t len : {size_t(0), size_t(2), size_t(55), size_t(64), size_t(10485760)}) {
@@ -131,6 +132,15 @@ int main() {
       threw = e.code() < 0;
     }
     expect(threw, "md5_bytes(NULL, 5) throws qsmd5::Error");
+  }
+  {
+    bool threw = false;
+    try {
+      qsmd5::content_md5_from_hex("xyz");
+    } catch (const qsmd5::Error&) {
+      threw = true;
+    }
+    expect(threw, "content_md5_from_hex rejects non-hex text");
   }
   std::printf("failures %d\n", failures);
   return failures ? 1 : 0;

@@ -63,6 +63,20 @@ def test_hex_matches_reference_format():
     assert qsmd5.hexdigest(b"\xff" * 16) == "f" * 32
 
 
+def test_base64_content_md5_header():
+    """RFC 1864 header form, checked against Python's base64 and RFC 1864's own
+    example digest (MD5 of "Check Integrity!" = Q2hlY2sgSW50ZWdyaXR5IQ==)."""
+    import base64
+    rng = random.Random(4)
+    for _ in range(200):
+        d = bytes(rng.getrandbits(8) for _ in range(16))
+        assert qsmd5.content_md5(d) == base64.b64encode(d).decode()
+    assert qsmd5.content_md5(b"Check Integrity!") == "Q2hlY2sgSW50ZWdyaXR5IQ=="
+    # the digest of "" (RFC 1321 A.5) in header form
+    assert qsmd5.content_md5(bytes.fromhex("d41d8cd98f00b204e9800998ecf8427e")) == \
+        "1B2M2Y8AsgTpgAmY7PhCfg=="
+
+
 def prepare_upload_restated(total, buf, min_part, threshold):
     """Direct restatement of QSTransferManager::PrepareUpload (QSTransferManager.cpp:492-546)."""
     if total < threshold:

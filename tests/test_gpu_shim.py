@@ -40,6 +40,8 @@ def test_cpp_dropin_shim():
     assert got["str_empty"] == h(b"")
     assert got["str_abc"] == h(b"abc")
     assert got["str_literal"] == h(b"message digest")
+    import base64
+    assert got["content_md5_abc"] == base64.b64encode(hashlib.md5(b"abc").digest()).decode()
     for L in (0, 2, 55, 64, 10485760):
         assert got["view_%d" % L] == h(bytes(lcg_bytes(12345, L + 100))[:L]), L
     assert got["streamtest_read1"] == h(b"01")
