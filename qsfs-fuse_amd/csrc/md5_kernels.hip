@@ -161,6 +161,12 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return v;
 }
 
+// Wave-uniform copy of a 32-bit value as UNSIGNED: the builtin returns int, and
+// widening that int to 64 bits would sign-extend (fatal for pointer halves).
+__device__ __forceinline__ uint32_t rfl_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
@@ -411,8 +417,7 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
   // ---------------- chain ----------------
   // Phases in which every live lane still has all kPcHalf blocks run without a
   // per-block lane predicate (wave-uniform branch on an SGPR).
-  const uint32_t live_phases = __builtin_amdgcn_readfirstlane(
-      wave_min_u32(t < n ? nblk : 0xffffffffu) / kPcHalf);
+  const uint32_t live_phases = rfl_u32(wave_min_u32(t < n ? nblk : 0xffffffffu) / kPcHalf);
   uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
   lds_barrier();
   for (uint32_t p = 0; p < phases; ++p) {
@@ -465,8 +470,7 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
     cd = chunks[idx];
   }
   const uint32_t nblk = (uint32_t)(cd.len >> 6);
-  const uint32_t ntiles =
-      __builtin_amdgcn_readfirstlane((wave_max_u32(nblk) + (kTB - 1)) / kTB);
+  const uint32_t ntiles = rfl_u32((wave_max_u32(nblk) + (kTB - 1)) / kTB);
   // Slot swizzle making the row reads (lane l reads row l) bank-conflict-free
   // for ds_read_b128's 16-lane groups: rows of 128 B alternate bank halves.
   auto swz = [](uint32_t c) -> uint32_t {

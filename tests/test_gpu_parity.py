@@ -324,3 +324,21 @@ def test_verify_etag_download_buffer():
     assert not qsmd5.verify_etag(data[:-1], etag)
     with pytest.raises(qsmd5.Md5Error):
         qsmd5.verify_etag(data, etag[:-2] + '-2"')
+
+
+def test_large_batches_select_throughput_kernels():
+    """> 16 384 chunks through the synchronous API: staged host chunks (aligned ->
+    coalesced kernel) and unaligned device chunks (one-wave kernel)."""
+    os.environ.pop("QSMD5_KERNEL", None)
+    import random
+    rng = random.Random(8)
+    n = 17000
+    host = lcg_bytes(71, 4 << 20)
+    base = ctypes.addressof(host)
+    spans = [(rng.randrange(0, (4 << 20) - 5000), rng.randrange(0, 5000)) for _ in range(n)]
+    want = md5_many([(base + o, L) for o, L in spans])
+    assert qsmd5.hash_batch([(base + o, L) for o, L in spans]) == want
+    dev = torch.frombuffer(bytearray(bytes(host)), dtype=torch.uint8).cuda()
+    odd = [(o | 1, L) for o, L in spans]
+    want_odd = md5_many([(base + o, L) for o, L in odd])
+    assert qsmd5.hash_batch([(dev.data_ptr() + o, L) for o, L in odd]) == want_odd
