@@ -360,22 +360,45 @@ extern "C" __global__ __launch_bounds__(256) void qsmd5_lcg_fill_kernel(
   }
 }
 
-// Latency-regime batch kernel (B up to one resident round, 256 x 64 chunks):
-// see the producer/consumer notes at kPcHalf.
-extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
-    const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
-    uint32_t* __restrict__ digests) {
+// Latency-regime batch kernel body (B up to one resident round, 256 x 64
+// chunks): see the producer/consumer notes at kPcHalf.
+//
+// kColumn = false: chunks[order[t]] is a whole chunk; digest -> digests[idx].
+// kColumn = true (column-pipelined host batches, qsmd5_runtime.cpp): the batch
+// is cut into columns [col_off, col_off + col_w) of every chunk.  chunks[t] is
+// lane t's staged SEGMENT {ptr = segment start, len = the chunk's TOTAL
+// length L} and idx = order[t] names the chunk.  A lane resumes from
+// states[idx] (or the MD5 IV when col_off == 0), runs the segment's blocks,
+// and then either parks the state (L - col_off > col_w) or finishes with the
+// tail and the full length L (MD5.cpp:279-312 over the whole message).
+// col_off and col_w are multiples of 64, so block boundaries line up.
+template <bool kColumn>
+__device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
+                                        const uint32_t* __restrict__ order, uint32_t n,
+                                        uint32_t* __restrict__ digests, uint64_t col_off,
+                                        uint64_t col_w, uint32_t* __restrict__ states) {
   __shared__ u32x4 ring[kPcSlots][16][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t t = blockIdx.x * 64u + lane;
   uint32_t idx = 0;
   ChunkDesc cd = {nullptr, 0};
+  uint64_t seg = 0;     // message bytes of this lane's segment
+  bool final = true;    // this segment ends the chunk
   if (t < n) {
-    idx = order ? order[t] : t;
-    cd = chunks[idx];
+    if (kColumn) {
+      idx = order[t];
+      cd = chunks[t];
+      const uint64_t rest = cd.len - col_off;
+      final = rest <= col_w;
+      seg = final ? rest : col_w;
+    } else {
+      idx = order ? order[t] : t;
+      cd = chunks[idx];
+      seg = cd.len;
+    }
   }
-  const uint32_t nblk = (uint32_t)(cd.len >> 6);
+  const uint32_t nblk = (uint32_t)(seg >> 6);
   const uint32_t phases = (wave_max_u32(nblk) + kPcHalf - 1) / kPcHalf;
   const uintptr_t pa = reinterpret_cast<uintptr_t>(cd.ptr);
   const uint32_t off = (uint32_t)(pa & 3u);
@@ -419,6 +442,13 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
   // per-block lane predicate (wave-uniform branch on an SGPR).
   const uint32_t live_phases = rfl_u32(wave_min_u32(t < n ? nblk : 0xffffffffu) / kPcHalf);
   uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  if (kColumn && col_off != 0 && t < n) {
+    const u32x4 s4 = *reinterpret_cast<const u32x4*>(states + 4u * (uint64_t)idx);
+    st[0] = s4.x;
+    st[1] = s4.y;
+    st[2] = s4.z;
+    st[3] = s4.w;
+  }
   lds_barrier();
   for (uint32_t p = 0; p < phases; ++p) {
     const uint32_t s0 = (p & 1u) * kPcHalf;
@@ -429,9 +459,27 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
     lds_barrier();
   }
   if (t >= n) return;
-  finish(st, cd.ptr + ((uint64_t)nblk << 6), (uint32_t)(cd.len & 63u), cd.len);
+  if (kColumn && !final) {
+    u32x4 o = {st[0], st[1], st[2], st[3]};
+    *reinterpret_cast<u32x4*>(states + 4u * (uint64_t)idx) = o;
+    return;
+  }
+  finish(st, cd.ptr + ((uint64_t)nblk << 6), (uint32_t)(seg & 63u), cd.len);
   u32x4 o = {st[0], st[1], st[2], st[3]};
   *reinterpret_cast<u32x4*>(digests + 4u * (uint64_t)idx) = o;
+}
+
+extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
+    const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
+    uint32_t* __restrict__ digests) {
+  pc_body<false>(chunks, order, n, digests, 0, ~0ull, nullptr);
+}
+
+extern "C" __global__ __launch_bounds__(128) void qsmd5_column_pc_kernel(
+    const ChunkDesc* __restrict__ segs, const uint32_t* __restrict__ order, uint32_t n,
+    uint32_t* __restrict__ digests, uint64_t col_off, uint64_t col_w,
+    uint32_t* __restrict__ states) {
+  pc_body<true>(segs, order, n, digests, col_off, col_w, states);
 }
 
 // ---------------------------------------------------------------------------
@@ -578,6 +626,15 @@ hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, u
     hipLaunchKernelGGL(qsmd5_batch_kernel, dim3(groups), dim3(64), 0, s,
                        static_cast<const ChunkDesc*>(chunks), order, n, digests);
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_column(const void* segs, const uint32_t* order, uint32_t n, uint32_t* digests,
+                         uint64_t col_off, uint64_t col_w, uint32_t* states, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(qsmd5_column_pc_kernel, dim3((n + 63u) / 64u), dim3(128), 0, s,
+                     static_cast<const ChunkDesc*>(segs), order, n, digests, col_off, col_w,
+                     states);
   return hipGetLastError();
 }
 

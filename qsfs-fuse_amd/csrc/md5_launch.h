@@ -21,6 +21,12 @@ constexpr uint32_t kLatencyKernelResident = 256u * 64u;
 // digests: device, 16 B per chunk indexed by chunk index.
 hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
                         int kind, hipStream_t s);
+// Column-pipelined latency kernel: lane t hashes segment segs[t] = {staged
+// start of bytes [col_off, col_off + col_w) of chunk order[t], that chunk's
+// total length}; state parks in states[4 * order[t]] between columns and the
+// digest lands in digests[4 * order[t]] after the chunk's last column.
+hipError_t launch_column(const void* segs, const uint32_t* order, uint32_t n, uint32_t* digests,
+                         uint64_t col_off, uint64_t col_w, uint32_t* states, hipStream_t s);
 hipError_t launch_blocks(uint32_t* state, const uint8_t* p, uint32_t nblk, hipStream_t s);
 hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint64_t total_len,
                         hipStream_t s);

@@ -144,7 +144,7 @@ struct Runtime {
   hipStream_t copy[kMaxCopyStreams] = {};
   int ncopy = 2;  // H2D streams (QSMD5_COPY_STREAMS), slices alternate over them
   hipStream_t compute[kComputeStreams] = {};
-  DevBuf d_desc, d_order, d_dig, d_staging;
+  DevBuf d_desc, d_order, d_dig, d_staging, d_state;
   HostPinned h_desc, h_order, h_dig;
   uint64_t staging_cap = kDefaultStaging;
   double last_wall_ms = 0, last_kernel_ms = 0;
@@ -237,13 +237,32 @@ int kernel_choice(size_t n, bool aligned16) {
   return aligned16 ? kKernelCoalesced : kKernelThroughput;
 }
 
+// Host-resident chunks are staged in SLICES.  Chunks (sorted by length) form
+// GROUPS that fit one staging region; a group is cut into COLUMNS of width W:
+// column j of a group is bytes [jW, (j+1)W) of each of its chunks still that
+// long.  One slice = one (group, column): one H2D transfer into a ring region,
+// then one kernel launch that resumes each chain from its parked state.
+// Columns let every chain start as soon as the first column lands, so the
+// serial chain of the LAST chunk copied no longer trails the transfer: only
+// its last column (~8 ms at W ~ 1 MiB) does.  W = ~0 (chunks no longer than
+// the column) degenerates to whole-chunk row slices.
+struct Group {
+  size_t first, count;  // range in host_idx
+  uint32_t ncols;
+};
 struct Slice {
-  size_t first, count;  // range in the host-chunk order list
-  uint64_t bytes;
+  size_t group;
+  uint32_t col;
+  size_t active;  // chunks of the group still live in this column (a prefix)
+  size_t seg0;    // first entry in the segment/order arrays (multi-column groups)
 };
 
-// The synchronous batch: device chunks in one launch; host chunks sliced,
-// staged and hashed with copy/compute overlap.  Caller holds rt().mu.
+constexpr uint64_t kColGrain = 64ull << 10;  // automatic column widths are multiples of this
+constexpr uint64_t kColMin = 1ull << 20;     // ... and at least this (>= 1 MiB per-chunk copies)
+constexpr uint64_t kNoColumns = ~0ull;
+
+// The synchronous batch: device chunks in one launch; host chunks staged in
+// slices with copy/compute overlap.  Caller holds rt().mu.
 int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
   Runtime& r = rt();
   auto t0 = std::chrono::steady_clock::now();
@@ -273,21 +292,59 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   std::sort(dev_idx.begin(), dev_idx.end(), by_len);
   std::sort(host_idx.begin(), host_idx.end(), by_len);
 
-  // Slices of host chunks and their staging regions.
+  // Column width: one column of every host chunk should fill about one slice.
   const uint64_t slice_target = env_u64(
       "QSMD5_SLICE_BYTES", std::min(kSliceMax, std::max(kSliceMin, host_total / 4)));
-  const uint64_t region = std::max<uint64_t>(slice_target, stage_bytes(max_host));
-  std::vector<Slice> slices;
+  uint64_t W = kNoColumns;
+  if (!host_idx.empty()) {
+    const uint64_t per = slice_target / host_idx.size();
+    uint64_t w = per > kSkew + kAlign ? (per - kSkew - kAlign) / kColGrain * kColGrain : 0;
+    w = std::max(w, kColMin);
+    if (const char* ev = getenv("QSMD5_COLUMN_BYTES"); ev && *ev) {
+      const uint64_t forced = env_u64("QSMD5_COLUMN_BYTES", 0);  // 0 = whole chunks
+      w = forced ? std::max<uint64_t>(64, forced & ~63ull) : kNoColumns;
+    }
+    if (w < max_host) W = w;
+  }
+  auto col_bytes = [&](uint64_t L, uint32_t j) -> uint64_t {  // chunk bytes in column j
+    if (W == kNoColumns) return j == 0 ? L : 0;
+    const uint64_t o = (uint64_t)j * W;
+    return L > o ? std::min(W, L - o) : 0;
+  };
+  // A region holds one column of a whole group.  When the column width sits at
+  // its floor (kColMin) the host chunks' first columns may overshoot the slice
+  // target slightly; grow the region (up to half the staging ring) rather than
+  // splitting off a small second group whose columns would all trail the first.
+  uint64_t first_cols = 0;
+  for (uint32_t ci : host_idx) first_cols += stage_bytes(col_bytes(len[ci], 0));
+  const uint64_t region = std::max<uint64_t>(
+      {slice_target, stage_bytes(col_bytes(max_host, 0)),
+       W == kNoColumns ? 0 : std::min<uint64_t>(first_cols, r.staging_cap / 2)});
+  std::vector<Group> groups;
   for (size_t k = 0; k < host_idx.size();) {
-    Slice s{k, 0, 0};
+    Group g{k, 0, 1};
+    uint64_t bytes = 0;
     while (k < host_idx.size()) {
-      uint64_t L = stage_bytes(len[host_idx[k]]);
-      if (s.count > 0 && s.bytes + L > region) break;
-      s.bytes += L;
-      ++s.count;
+      const uint64_t b = stage_bytes(col_bytes(len[host_idx[k]], 0));
+      if (g.count > 0 && bytes + b > region) break;
+      bytes += b;
+      ++g.count;
       ++k;
     }
-    slices.push_back(s);
+    const uint64_t longest = len[host_idx[g.first]];
+    if (W != kNoColumns) g.ncols = (uint32_t)std::max<uint64_t>(1, (longest + W - 1) / W);
+    groups.push_back(g);
+  }
+  std::vector<Slice> slices;
+  size_t nseg = 0;
+  for (size_t gi = 0; gi < groups.size(); ++gi) {
+    const Group& g = groups[gi];
+    for (uint32_t j = 0; j < g.ncols; ++j) {
+      size_t act = 0;
+      while (act < g.count && col_bytes(len[host_idx[g.first + act]], j) > 0) ++act;
+      slices.push_back(Slice{gi, j, act, nseg});
+      if (g.ncols > 1) nseg += act;
+    }
   }
   size_t nregions = 0;
   if (!slices.empty()) {
@@ -297,24 +354,40 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
     if (int rc = r.d_staging.reserve(nregions * region)) return rc;
   }
 
-  // Descriptors (device pointers) for every chunk, upfront.
-  if (int rc = r.h_desc.reserve(n * sizeof(qsmd5_chunk) + 16)) return rc;
-  if (int rc = r.h_order.reserve(n * sizeof(uint32_t) + 16)) return rc;
+  // Descriptors (device pointers) for every chunk, upfront; segment
+  // descriptors and lane->chunk maps for the multi-column slices behind them.
+  const size_t meta_bytes = n * sizeof(qsmd5_chunk) + nseg * sizeof(qsmd5_chunk);
+  const size_t order_words = n + nseg;
+  if (int rc = r.h_desc.reserve(meta_bytes + 16)) return rc;
+  if (int rc = r.h_order.reserve(order_words * sizeof(uint32_t) + 16)) return rc;
   if (int rc = r.h_dig.reserve(n * 16 + 16)) return rc;
-  if (int rc = r.d_desc.reserve(n * sizeof(qsmd5_chunk) + 16)) return rc;
-  if (int rc = r.d_order.reserve(n * sizeof(uint32_t) + 16)) return rc;
+  if (int rc = r.d_desc.reserve(meta_bytes + 16)) return rc;
+  if (int rc = r.d_order.reserve(order_words * sizeof(uint32_t) + 16)) return rc;
   if (int rc = r.d_dig.reserve(n * 16 + 16)) return rc;
+  if (nseg)
+    if (int rc = r.d_state.reserve(n * 16 + 16)) return rc;
   qsmd5_chunk* hd = static_cast<qsmd5_chunk*>(r.h_desc.p);
+  qsmd5_chunk* hseg = hd + n;
   uint32_t* ho = static_cast<uint32_t*>(r.h_order.p);
+  uint32_t* hso = ho + n;
   for (size_t i = 0; i < n; ++i) hd[i] = {len[i] ? chunks[i].ptr : nullptr, len[i]};
   uint8_t* stage = static_cast<uint8_t*>(r.d_staging.p);
+  std::vector<uint8_t*> slice_base(slices.size());
   for (size_t si = 0; si < slices.size(); ++si) {
+    const Slice& sl = slices[si];
+    const Group& g = groups[sl.group];
     uint8_t* base = stage + (si % nregions) * region;
+    slice_base[si] = base;
     uint64_t off = 0;
-    for (size_t k = 0; k < slices[si].count; ++k) {
-      uint32_t ci = host_idx[slices[si].first + k];
-      hd[ci].ptr = base + off;
-      off += stage_bytes(len[ci]);
+    for (size_t k = 0; k < sl.active; ++k) {
+      const uint32_t ci = host_idx[g.first + k];
+      if (g.ncols > 1) {
+        hseg[sl.seg0 + k] = {base + off, len[ci]};
+        hso[sl.seg0 + k] = ci;
+      } else {
+        hd[ci].ptr = base + off;
+      }
+      off += stage_bytes(col_bytes(len[ci], sl.col));
     }
   }
   size_t pos = 0;
@@ -330,22 +403,33 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
     for (hipStream_t s : r.compute) (void)hipStreamSynchronize(s);
     return code;
   };
-  QS_HIP(hipMemcpyAsync(r.d_desc.p, hd, n * sizeof(qsmd5_chunk), hipMemcpyHostToDevice, s0));
-  QS_HIP(hipMemcpyAsync(r.d_order.p, ho, n * sizeof(uint32_t), hipMemcpyHostToDevice, s0));
+  QS_HIP(hipMemcpyAsync(r.d_desc.p, hd, meta_bytes, hipMemcpyHostToDevice, s0));
+  QS_HIP(hipMemcpyAsync(r.d_order.p, ho, order_words * sizeof(uint32_t), hipMemcpyHostToDevice, s0));
   hipEvent_t meta_ready = nullptr, k_first = nullptr, k_last = nullptr;
   if (int rc = events.make(&meta_ready, hipEventDisableTiming)) return drain(rc);
   if (int rc = events.make(&k_first, hipEventDefault)) return drain(rc);
   if (int rc = events.make(&k_last, hipEventDefault)) return drain(rc);
   QS_HIP(hipEventRecord(meta_ready, s0));
   std::vector<hipEvent_t> region_free(nregions, nullptr);
+  // QSMD5_TRACE=1: per-slice copy/kernel timeline on stderr (diagnostics).
+  const bool trace = env_u64("QSMD5_TRACE", 0) != 0;
+  std::vector<hipEvent_t> tr(trace ? 4 * slices.size() + 1 : 0, nullptr);
+  for (auto& ev : tr)
+    if (int rc = events.make(&ev, hipEventDefault)) return drain(rc);
+  if (trace) QS_HIP(hipEventRecord(tr.back(), s0));
   const uint32_t* d_order = static_cast<const uint32_t*>(r.d_order.p);
+  const qsmd5_chunk* d_seg = static_cast<const qsmd5_chunk*>(r.d_desc.p) + n;
   uint32_t* d_dig = static_cast<uint32_t*>(r.d_dig.p);
   bool first_kernel = true;
-  auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt, bool aligned16) -> int {
+  auto mark_first = [&](hipStream_t s) -> int {
     if (first_kernel) {
       QS_HIP(hipEventRecord(k_first, s));
       first_kernel = false;
     }
+    return 0;
+  };
+  auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt, bool aligned16) -> int {
+    if (int rc = mark_first(s)) return rc;
     hipError_t e = qsmd5::launch_batch(r.d_desc.p, ord, (uint32_t)cnt, d_dig,
                                        kernel_choice(cnt, aligned16), s);
     if (e != hipSuccess) return hip_fail(e, "qsmd5 kernel launch");
@@ -359,35 +443,76 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
       aligned16 = aligned16 && (reinterpret_cast<uintptr_t>(hd[ci].ptr) & 15u) == 0;
     if (int rc = launch(s0, d_order, dev_idx.size(), aligned16)) return drain(rc);
   }
-  // Host-resident slices: H2D on the copy stream into the slice's ring region
-  // (after the kernel that last used the region), then a launch on its own
-  // compute stream once the copy and the descriptors have landed.
+  // Host-resident slices: H2D on a copy stream into the slice's ring region
+  // (after the kernel that last used the region), then a launch on its group's
+  // compute stream (so a group's columns run in order) once the copy and the
+  // descriptors have landed.  Runs of equal-length chunks at a constant host
+  // stride (a file's parts) go as one 2-D copy per column.
   for (size_t si = 0; si < slices.size(); ++si) {
+    const Slice& sl = slices[si];
+    const Group& g = groups[sl.group];
     const size_t reg = si % nregions;
-    hipStream_t cs = r.compute[1 + si % (kComputeStreams - 1)];
+    hipStream_t cs = r.compute[1 + sl.group % (kComputeStreams - 1)];
     hipStream_t cp = r.copy[si % r.ncopy];
     if (region_free[reg]) {
       hipError_t e = hipStreamWaitEvent(cp, region_free[reg], 0);
       if (e != hipSuccess) return drain(hip_fail(e, "hipStreamWaitEvent"));
     }
-    for (size_t k = 0; k < slices[si].count; ++k) {
-      uint32_t ci = host_idx[slices[si].first + k];
-      if (len[ci] == 0) continue;
-      hipError_t e = hipMemcpyAsync(const_cast<void*>(hd[ci].ptr), chunks[ci].ptr, len[ci],
-                                    hipMemcpyHostToDevice, cp);
+    const uint64_t col_off = W == kNoColumns ? 0 : (uint64_t)sl.col * W;
+    uint8_t* dst = slice_base[si];
+    if (trace) QS_HIP(hipEventRecord(tr[4 * si], cp));
+    for (size_t k = 0; k < sl.active;) {
+      const uint32_t ci = host_idx[g.first + k];
+      const uint64_t w = col_bytes(len[ci], sl.col);
+      const uint8_t* src = static_cast<const uint8_t*>(chunks[ci].ptr) + col_off;
+      size_t rows = 1;
+      int64_t stride = 0;
+      if (k + 1 < sl.active) {
+        const uint32_t c1 = host_idx[g.first + k + 1];
+        stride = static_cast<const uint8_t*>(chunks[c1].ptr) -
+                 static_cast<const uint8_t*>(chunks[ci].ptr);
+        if (len[c1] == len[ci] && stride >= (int64_t)w && stride < (1ll << 40)) {
+          while (k + rows < sl.active) {
+            const uint32_t cr = host_idx[g.first + k + rows];
+            const uint32_t cq = host_idx[g.first + k + rows - 1];
+            if (len[cr] != len[ci] || static_cast<const uint8_t*>(chunks[cr].ptr) -
+                                              static_cast<const uint8_t*>(chunks[cq].ptr) != stride)
+              break;
+            ++rows;
+          }
+        }
+      }
+      hipError_t e;
+      if (rows > 1)
+        e = hipMemcpy2DAsync(dst, stage_bytes(w), src, (size_t)stride, w, rows,
+                             hipMemcpyHostToDevice, cp);
+      else
+        e = hipMemcpyAsync(dst, src, w, hipMemcpyHostToDevice, cp);
       if (e != hipSuccess) return drain(hip_fail(e, "hipMemcpyAsync H2D"));
+      dst += rows * stage_bytes(w);
+      k += rows;
     }
     hipEvent_t copied = nullptr, done = nullptr;
     if (int rc = events.make(&copied, hipEventDisableTiming)) return drain(rc);
     if (int rc = events.make(&done, hipEventDisableTiming)) return drain(rc);
+    if (trace) QS_HIP(hipEventRecord(tr[4 * si + 1], cp));
     hipError_t e = hipEventRecord(copied, cp);
     if (e == hipSuccess) e = hipStreamWaitEvent(cs, copied, 0);
     if (e == hipSuccess) e = hipStreamWaitEvent(cs, meta_ready, 0);
     if (e != hipSuccess) return drain(hip_fail(e, "stream ordering"));
-    // staged chunks sit at 256-B-aligned offsets plus a 16-B-multiple skew
-    if (int rc = launch(cs, d_order + dev_idx.size() + slices[si].first, slices[si].count, true))
-      return drain(rc);
+    if (trace) QS_HIP(hipEventRecord(tr[4 * si + 2], cs));
+    if (g.ncols > 1) {
+      if (int rc = mark_first(cs)) return drain(rc);
+      e = qsmd5::launch_column(d_seg + sl.seg0, d_order + n + sl.seg0, (uint32_t)sl.active, d_dig,
+                               col_off, W, static_cast<uint32_t*>(r.d_state.p), cs);
+      if (e != hipSuccess) return drain(hip_fail(e, "qsmd5 column kernel launch"));
+    } else {
+      // staged chunks sit at 256-B-aligned offsets plus a 16-B-multiple skew
+      if (int rc = launch(cs, d_order + dev_idx.size() + g.first, sl.active, true))
+        return drain(rc);
+    }
     if ((e = hipEventRecord(done, cs)) != hipSuccess) return drain(hip_fail(e, "hipEventRecord"));
+    if (trace) QS_HIP(hipEventRecord(tr[4 * si + 3], cs));
     region_free[reg] = done;
   }
   // Join every compute stream into s0, then fetch the digests.
@@ -403,6 +528,16 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   hipError_t e = hipStreamSynchronize(s0);
   if (e != hipSuccess) return drain(hip_fail(e, "hipStreamSynchronize"));
   memcpy(digests, r.h_dig.p, n * 16);
+  if (trace) {
+    fprintf(stderr, "qsmd5 trace: %zu slices, column width %llu, %zu groups, %zu regions\n",
+            slices.size(), (unsigned long long)(W == kNoColumns ? 0 : W), groups.size(), nregions);
+    for (size_t si = 0; si < slices.size(); ++si) {
+      float t[4] = {0, 0, 0, 0};
+      for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&t[k], tr.back(), tr[4 * si + k]);
+      fprintf(stderr, "  slice %zu g%zu c%u n=%zu copy %.2f..%.2f ms kernel %.2f..%.2f ms\n", si,
+              slices[si].group, slices[si].col, slices[si].active, t[0], t[1], t[2], t[3]);
+    }
+  }
   float kms = 0;
   r.last_kernel_ms =
       (!first_kernel && hipEventElapsedTime(&kms, k_first, k_last) == hipSuccess) ? kms : 0.0;

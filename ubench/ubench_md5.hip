@@ -404,6 +404,74 @@ static void run_stream_read(uint64_t bytes, int reps) {
   CK(hipFree(sink));
 }
 
+// Raw H2D bandwidth from pinned host memory: the ceiling for host-resident
+// batches (BASELINE config 3).  `total` bytes in `piece`-sized copies
+// alternating over `nstreams` streams.
+static void run_h2d(size_t total, size_t piece, int nstreams) {
+  void* h = nullptr;
+  void* d = nullptr;
+  CK(hipHostMalloc(&h, total, hipHostMallocDefault));
+  CK(hipMalloc(&d, total));
+  memset(h, 1, total);
+  hipStream_t st[4];
+  for (int i = 0; i < nstreams; ++i) CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+  double best = 1e30;
+  for (int r = 0; r < 3; ++r) {
+    CK(hipDeviceSynchronize());
+    auto t0 = std::chrono::steady_clock::now();
+    int k = 0;
+    for (size_t o = 0; o < total; o += piece, ++k)
+      CK(hipMemcpyAsync((char*)d + o, (char*)h + o, std::min(piece, total - o),
+                        hipMemcpyHostToDevice, st[k % nstreams]));
+    CK(hipDeviceSynchronize());
+    double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    best = std::min(best, s);
+  }
+  printf("h2d total=%.1f GiB piece=%.0f MiB streams=%d: %.3f s -> %.2f GiB/s (%.1f GB/s)\n",
+         total / 1073741824.0, piece / 1048576.0, nstreams, best, total / 1073741824.0 / best,
+         total / 1e9 / best);
+  for (int i = 0; i < nstreams; ++i) CK(hipStreamDestroy(st[i]));
+  CK(hipFree(d));
+  CK(hipHostFree(h));
+}
+
+// Column copies: `rows` chunks of `len` bytes at host stride `len`, copied as
+// columns of `width` bytes per chunk with one hipMemcpy2DAsync per column
+// (device pitch = len + skew) -- the H2D pattern of a column-pipelined batch.
+static void run_h2d_2d(int rows, size_t len, size_t width, int nstreams) {
+  const size_t skew = 4352;
+  const size_t total = (size_t)rows * len;
+  void* h = nullptr;
+  void* d = nullptr;
+  CK(hipHostMalloc(&h, total, hipHostMallocDefault));
+  CK(hipMalloc(&d, (size_t)rows * (len + skew)));
+  memset(h, 1, total);
+  hipStream_t st[4];
+  for (int i = 0; i < nstreams; ++i) CK(hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking));
+  double best = 1e30;
+  for (int r = 0; r < 3; ++r) {
+    CK(hipDeviceSynchronize());
+    auto t0 = std::chrono::steady_clock::now();
+    int k = 0;
+    for (size_t o = 0; o < len; o += width, ++k)
+      CK(hipMemcpy2DAsync((char*)d + o, len + skew, (char*)h + o, len, std::min(width, len - o),
+                          rows, hipMemcpyHostToDevice, st[k % nstreams]));
+    CK(hipDeviceSynchronize());
+    double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    best = std::min(best, s);
+  }
+  // spot-check placement
+  std::vector<uint8_t> probe(16);
+  CK(hipMemcpy(probe.data(), (char*)d + (size_t)(rows - 1) * (len + skew) + len - 16, 16,
+               hipMemcpyDeviceToHost));
+  printf("h2d-2d rows=%d len=%.1f MiB width=%.2f MiB streams=%d: %.3f s -> %.2f GiB/s (%.1f GB/s)%s\n",
+         rows, len / 1048576.0, width / 1048576.0, nstreams, best, total / 1073741824.0 / best,
+         total / 1e9 / best, probe[15] == 1 ? "" : "  PLACEMENT WRONG");
+  for (int i = 0; i < nstreams; ++i) CK(hipStreamDestroy(st[i]));
+  CK(hipFree(d));
+  CK(hipHostFree(h));
+}
+
 int main(int argc, char** argv) {
   const char* mode = argc > 1 ? argv[1] : "all";
   if (!strcmp(mode, "calib")) {
@@ -411,6 +479,18 @@ int main(int argc, char** argv) {
     run_stream_read(4ull << 30, 2);
     run_md5(512, 10485760, 1, false, 1);
     run_md5(131072, 65536, 1, false, 0);
+    return 0;
+  }
+  if (!strcmp(mode, "h2d")) {
+    const size_t G = 1ull << 30;
+    for (int ns : {1, 2, 4})
+      for (size_t piece : {G / 16, 1 * G, 4 * G}) run_h2d(16 * G, piece, ns);
+    run_h2d(40 * G, 4 * G, 2);
+    for (size_t w : {256ull << 10, 1ull << 20, 10ull << 19})
+      for (int ns : {1, 2}) run_h2d_2d(4096, 10 << 20, w, ns);
+    // per-chunk 10 MiB copies, as the row-sliced pipeline issues them
+    for (int ns : {1, 2}) run_h2d(40 * G, 10ull << 20, ns);
+    for (int ns : {1, 2}) run_h2d(4 * G, 1ull << 20, ns);
     return 0;
   }
   if (!strcmp(mode, "zc")) {
