@@ -499,6 +499,37 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_column_pc_kernel(
 #define QS_GP(p) ((const __attribute__((address_space(1))) void*)(uintptr_t)(p))
 #define QS_LP(p) ((__attribute__((address_space(3))) void*)(uintptr_t)(uint32_t)(uintptr_t)(p))
 
+// One fast-region tile U of a group (see batch_coal_body): prefetch the next
+// tile from each instruction's source pointer into buffer (U + 1) & 1 and
+// advance the pointer, then compress tile U from buffer U & 1 with no lane
+// predicate.  The DMA immediate offset is NOT usable to step through a chunk:
+// the hardware adds it to the LDS destination as well as to the global address.
+template <int U, int kU, int kTB, int kS, int kCPI>
+__device__ __forceinline__ void coal_fast_group(uint32_t (&st)[4], const uint8_t* (&gp)[kS],
+                                                u32x4 (*tile_buf)[64][kS], uint32_t lane,
+                                                uint32_t rswz) {
+  if constexpr (U < kU) {
+#pragma unroll
+    for (int i = 0; i < kS; ++i) {
+      __builtin_amdgcn_global_load_lds(QS_GP(gp[i]), QS_LP(&tile_buf[(U + 1) & 1][i * kCPI][0]), 16,
+                                       0, 0);
+      gp[i] += kTB * 64;
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kS) : "memory");
+#pragma unroll
+    for (int h = 0; h < kTB; ++h) {
+      uint32_t w[16];
+      unpack4(w, 0, tile_buf[U & 1][lane][(4 * h + 0) ^ rswz]);
+      unpack4(w, 1, tile_buf[U & 1][lane][(4 * h + 1) ^ rswz]);
+      unpack4(w, 2, tile_buf[U & 1][lane][(4 * h + 2) ^ rswz]);
+      unpack4(w, 3, tile_buf[U & 1][lane][(4 * h + 3) ^ rswz]);
+      md5_compress(st, w);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    coal_fast_group<U + 1, kU, kTB, kS, kCPI>(st, gp, tile_buf, lane, rswz);
+  }
+}
+
 template <int kTB, int kBufs>
 __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ chunks,
                                                 const uint32_t* __restrict__ order, uint32_t n,
@@ -557,7 +588,25 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
 #pragma unroll
   for (int k = 0; k < kBufs - 1; ++k)
     if ((uint32_t)k < ntiles) issue_tile((uint32_t)k, (uint32_t)k);
-  for (uint32_t tl = 0; tl < ntiles; ++tl) {
+  uint32_t tl = 0;
+  if constexpr (kBufs == 2) {
+    // Fast region: a full wave whose every chain still has whole tiles.  No
+    // clamp, no dummy source, no per-block lane predicate: each DMA source is
+    // one 64-bit pointer bumped per tile (1 VALU), and the row reads are
+    // loop-invariant per-lane addresses.  This removes ~24 VALU per block
+    // (352 -> 328, ~7%) in a regime bound by VALU x clock
+    // (profiles/r01_ubench_probe.log).
+    constexpr int kU = 2;  // tiles per loop trip: keeps the buffer index static
+    const bool full_wave = (blockIdx.x + 1u) * 64u <= n;
+    const uint32_t fast_tiles = full_wave ? rfl_u32(wave_min_u32(nblk)) / (uint32_t)kTB : 0u;
+    const uint8_t* gp[kS];  // source of tile tl + 1 for DMA instruction i
+#pragma unroll
+    for (int i = 0; i < kS; ++i)
+      gp[i] = src[i] + kTB * 64u + (piece[i] >> 2) * 64u + (piece[i] & 3u) * 16u;
+    for (; tl + (uint32_t)kU < fast_tiles; tl += (uint32_t)kU)
+      coal_fast_group<0, kU, kTB, kS, kCPI>(st, gp, tile_buf, lane, rswz);
+  }
+  for (; tl < ntiles; ++tl) {
     const uint32_t b = tl % kBufs;
     if (tl + (kBufs - 1) < ntiles) {
       issue_tile((tl + (kBufs - 1)) % kBufs, tl + (kBufs - 1));

@@ -472,6 +472,152 @@ static void run_h2d_2d(int rows, size_t len, size_t width, int nstreams) {
   CK(hipHostFree(h));
 }
 
+
+#define QS_GP(p) ((const __attribute__((address_space(1))) void*)(uintptr_t)(p))
+#define QS_LP(p) ((__attribute__((address_space(3))) void*)(uintptr_t)(uint32_t)(uintptr_t)(p))
+// ---- 3. throughput-kernel probes ---------------------------------------------
+// Copy of batch_coal_body<2,2> with a probe mode: 0 = as shipped, 1 = memory
+// only (compress replaced by an XOR fold), 2 = compute only (no LDS-DMA, the
+// tile buffers hold garbage).  Lane 0 stamps s_memtime / s_memrealtime at entry
+// and exit: clock = d(memtime) / d(realtime) x 100 MHz.
+template <int kMode>
+__global__ __launch_bounds__(64) void k_coal_probe(const ChunkDesc* __restrict__ chunks, uint32_t n,
+                                                   uint32_t* __restrict__ digests,
+                                                   uint64_t* __restrict__ stamps) {
+  constexpr int kTB = 2, kBufs = 2, kS = 8, kCPI = 8;
+  __shared__ u32x4 tile_buf[kBufs][64][kS];
+  const uint64_t m0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  const uint32_t lane = threadIdx.x;
+  const uint32_t t = blockIdx.x * 64u + lane;
+  ChunkDesc cd = {nullptr, 0};
+  if (t < n) cd = chunks[t];
+  const uint32_t nblk = (uint32_t)(cd.len >> 6);
+  const uint32_t ntiles = rfl_u32((wave_max_u32(nblk) + (kTB - 1)) / kTB);
+  auto swz = [](uint32_t c) -> uint32_t { return (c >> 1) & 7u; };
+  const uint32_t slot = lane % kS;
+  const uint64_t myptr = reinterpret_cast<uint64_t>(cd.ptr);
+  const uint8_t* src[kS];
+  uint32_t src_nblk[kS], piece[kS];
+#pragma unroll
+  for (int i = 0; i < kS; ++i) {
+    const int c = i * kCPI + (int)(lane / kS);
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)myptr, c, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(myptr >> 32), c, 64);
+    src[i] = reinterpret_cast<const uint8_t*>(((uint64_t)hi << 32) | lo);
+    src_nblk[i] = (uint32_t)__shfl((int)nblk, c, 64);
+    piece[i] = slot ^ swz((uint32_t)c);
+  }
+  const uint8_t* dummy = reinterpret_cast<const uint8_t*>(chunks);
+  auto issue_tile = [&](uint32_t b, uint32_t tl) {
+    if (kMode == 2) return;
+#pragma unroll
+    for (int i = 0; i < kS; ++i) {
+      const uint32_t blk = min(tl * (uint32_t)kTB + (piece[i] >> 2), src_nblk[i] - 1u);
+      const uint8_t* g = src_nblk[i] ? src[i] + (uint64_t)blk * 64u + (piece[i] & 3u) * 16u : dummy;
+      __builtin_amdgcn_global_load_lds(QS_GP(g), QS_LP(&tile_buf[b][i * kCPI][0]), 16, 0, 0);
+    }
+  };
+  const uint32_t rswz = swz(lane);
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  issue_tile(0, 0);
+  for (uint32_t tl = 0; tl < ntiles; ++tl) {
+    const uint32_t b = tl % kBufs;
+    if (tl + 1 < ntiles) {
+      issue_tile((tl + 1) % kBufs, tl + 1);
+      if (kMode != 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      if (kMode != 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#pragma unroll
+    for (int h = 0; h < kTB; ++h) {
+      u32x4 q0 = tile_buf[b][lane][(4 * h + 0) ^ rswz];
+      u32x4 q1 = tile_buf[b][lane][(4 * h + 1) ^ rswz];
+      u32x4 q2 = tile_buf[b][lane][(4 * h + 2) ^ rswz];
+      u32x4 q3 = tile_buf[b][lane][(4 * h + 3) ^ rswz];
+      if (tl * (uint32_t)kTB + h < nblk) {
+        if (kMode == 1) {
+          st[0] ^= q0.x ^ q1.y ^ q2.z ^ q3.w;
+          st[1] += q0.y ^ q1.z ^ q2.w ^ q3.x;
+          st[2] ^= q0.z + q1.w + q2.x + q3.y;
+          st[3] += q0.w + q1.x + q2.y + q3.z;
+        } else {
+          uint32_t w[16];
+          unpack4(w, 0, q0);
+          unpack4(w, 1, q1);
+          unpack4(w, 2, q2);
+          unpack4(w, 3, q3);
+          md5_compress(st, w);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if (t < n) {
+    u32x4 o = {st[0], st[1], st[2], st[3]};
+    *reinterpret_cast<u32x4*>(digests + 4u * (uint64_t)t) = o;
+  }
+  const uint64_t m1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) {
+    stamps[4 * blockIdx.x + 0] = m0;
+    stamps[4 * blockIdx.x + 1] = r0;
+    stamps[4 * blockIdx.x + 2] = m1;
+    stamps[4 * blockIdx.x + 3] = r1;
+  }
+}
+
+template <int kMode>
+static void run_coal_probe(int B, uint64_t L, uint64_t pad, int reps) {
+  uint64_t stride = ((L + 255) & ~uint64_t(255)) + pad;
+  uint8_t* d_data;
+  CK(hipMalloc(&d_data, stride * (uint64_t)B));
+  const uint64_t segs = (L + 1023) / 1024;
+  const uint64_t thr = segs * (uint64_t)B;
+  hipLaunchKernelGGL(qsmd5_lcg_fill_kernel, dim3((thr + 255) / 256), dim3(256), 0, 0, d_data,
+                     stride, L, 12345u, (uint32_t)B, segs);
+  std::vector<ChunkDesc> h(B);
+  for (int i = 0; i < B; ++i) h[i] = {d_data + stride * (uint64_t)i, L};
+  ChunkDesc* d_desc;
+  uint32_t* d_dig;
+  uint64_t* d_st;
+  const int grid = (B + 63) / 64;
+  CK(hipMalloc(&d_desc, sizeof(ChunkDesc) * B));
+  CK(hipMalloc(&d_dig, 16 * (size_t)B));
+  CK(hipMalloc(&d_st, 32 * (size_t)grid));
+  CK(hipMemcpy(d_desc, h.data(), sizeof(ChunkDesc) * B, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<float> ms(reps);
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(k_coal_probe<kMode>, dim3(grid), dim3(64), 0, 0, d_desc, (uint32_t)B, d_dig, d_st);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    CK(hipEventElapsedTime(&ms[r], e0, e1));
+  }
+  std::vector<uint64_t> st(4 * (size_t)grid);
+  CK(hipMemcpy(st.data(), d_st, 32 * (size_t)grid, hipMemcpyDeviceToHost));
+  std::vector<double> clk, dur;
+  for (int g = 0; g < grid; ++g) {
+    double dm = (double)(st[4 * g + 2] - st[4 * g]), dr = (double)(st[4 * g + 3] - st[4 * g + 1]);
+    if (dr > 0) clk.push_back(dm / dr * 100.0), dur.push_back(dr / 100.0);
+  }
+  std::sort(clk.begin(), clk.end());
+  std::sort(dur.begin(), dur.end());
+  std::vector<float> s = ms;
+  std::sort(s.begin(), s.end());
+  const double med = s[s.size() / 2];
+  printf("probe[%s] B=%d L=%llu pad=%llu: median %.3f ms best %.3f ms -> %.1f GB/s; wave clock median %.0f MHz "
+         "(p10 %.0f p90 %.0f); wave time median %.1f us max %.1f us\n",
+         kMode == 0 ? "full" : kMode == 1 ? "mem-only" : "compute-only", B, (unsigned long long)L,
+         (unsigned long long)pad, med, s[0], (double)L * B / (med * 1e-3) / 1e9, clk[clk.size() / 2],
+         clk[clk.size() / 10], clk[clk.size() * 9 / 10], dur[dur.size() / 2], dur.back());
+  CK(hipFree(d_data));
+  CK(hipFree(d_desc));
+  CK(hipFree(d_dig));
+  CK(hipFree(d_st));
+}
+
 int main(int argc, char** argv) {
   const char* mode = argc > 1 ? argv[1] : "all";
   if (!strcmp(mode, "calib")) {
@@ -556,6 +702,42 @@ int main(int argc, char** argv) {
     }
     run_md5(512, 32ull << 20, 2, false, 0, 0);
     run_md5(512, 32ull << 20, 2, false, 0, 4096);
+    return 0;
+  }
+  if (!strcmp(mode, "cross")) {
+    // latency (pc) vs coalesced kernel around the selection threshold (16384 chunks)
+    for (int B : {8192, 12288, 16384, 20480, 24576, 32768, 49152})
+      for (int w : {1, 2}) run_md5(B, 1 << 20, 3, false, w, 4352);
+    return 0;
+  }
+  if (!strcmp(mode, "coalfast")) {
+    // A/B: the previous coal body (probe copy, mode 0) vs the shipped kernel with the fast region
+    int bad = run_edges(2);
+    for (int rep = 0; rep < 2; ++rep) {
+      run_coal_probe<0>(131072, 65536, 4352, 5);
+      run_md5(131072, 65536, 5, rep == 0, 2, 4352);
+    }
+    run_coal_probe<0>(65536, 262144, 4352, 3);
+    run_md5(65536, 262144, 3, true, 2, 4352);
+    run_coal_probe<0>(32768, 1 << 20, 4352, 3);
+    run_md5(32768, 1 << 20, 3, true, 2, 4352);
+    run_md5(131072, 65536 + 64 * 3, 3, true, 2, 4352);
+    run_md5(100000, 65536 + 17 * 64, 3, true, 2, 4352);
+    return bad ? 1 : 0;
+  }
+  if (!strcmp(mode, "probe")) {
+    for (int rep = 0; rep < 2; ++rep) {
+      run_coal_probe<0>(131072, 65536, 4352, 5);
+      run_coal_probe<1>(131072, 65536, 4352, 5);
+      run_coal_probe<2>(131072, 65536, 4352, 5);
+    }
+    run_coal_probe<0>(65536, 262144, 4352, 3);
+    run_coal_probe<1>(65536, 262144, 4352, 3);
+    run_coal_probe<2>(65536, 262144, 4352, 3);
+    run_coal_probe<0>(262144, 65536, 4352, 3);
+    run_coal_probe<1>(262144, 65536, 4352, 3);
+    run_coal_probe<2>(262144, 65536, 4352, 3);
+    run_coal_probe<0>(8192, 1 << 20, 4352, 3);
     return 0;
   }
   if (!strcmp(mode, "sat")) {
