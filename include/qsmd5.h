@@ -33,6 +33,15 @@
  * device, so it is safe to call after fuse_main() has forked (reference
  * Operations.cpp:1520-1549 initialises threads after the fork for the same
  * reason).
+ *
+ * Multi-GPU (one process, e.g. the qsfs daemon): QSMD5_DEVICES="all" or a
+ * comma list of ordinals binds several GPUs at init.  qsmd5_hash_batch[_ex]
+ * then splits a batch: device chunks run on the GPU that holds them, and host
+ * chunks go in contiguous byte-balanced ranges to up to
+ * ceil(host bytes / QSMD5_SHARD_BYTES) GPUs (default 4 GiB per GPU), one
+ * thread per GPU.  A chunk in device memory of a GPU that is not bound is
+ * rejected with -EINVAL (a kernel cannot read it safely).  Streaming contexts,
+ * device-async batches and the fill helper use the first bound GPU.
  */
 #ifndef QSMD5_H_
 #define QSMD5_H_
@@ -75,8 +84,9 @@ typedef struct qsmd5_part {
 #define QSMD5_FLAG_REF_TRUNCATE32 1 /* hash only len mod 2^32 bytes, like MD5(std::string) */
 #define QSMD5_FLAG_ALIGNED16 2      /* device_async_ex: caller promises 16-B-aligned chunk ptrs */
 
-/* Initialise the runtime on the current HIP device (idempotent).  Returns 0,
- * or -ENODEV when no GPU is usable. */
+/* Initialise the runtime on the current HIP device, or on the QSMD5_DEVICES
+ * list (idempotent).  Returns 0, -ENODEV when no GPU is usable or the list
+ * names a missing GPU, or -EINVAL when the list is malformed. */
 QSMD5_API int qsmd5_init(int flags);
 
 QSMD5_API int qsmd5_abi_version(void);

@@ -29,6 +29,7 @@
 #include <new>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/qsmd5.h"
@@ -136,10 +137,10 @@ struct EventSet {
   }
 };
 
-struct Runtime {
-  std::mutex mu;  // serialises batches on the device
-  bool ready = false;
-  int init_rc = 0;
+// One bound GPU: its streams, scratch and staging ring.  Batches on one Dev are
+// serialised by its mutex; different Devs run concurrently (multi-GPU shards).
+struct Dev {
+  std::mutex mu;
   int device = -1;
   hipStream_t copy[kMaxCopyStreams] = {};
   int ncopy = 2;  // H2D streams (QSMD5_COPY_STREAMS), slices alternate over them
@@ -150,12 +151,72 @@ struct Runtime {
   double last_wall_ms = 0, last_kernel_ms = 0;
 };
 
+struct Runtime {
+  bool ready = false;
+  int init_rc = 0;
+  std::vector<Dev*> devs;       // devs[0] = primary (ctx, device-async, fill)
+  uint64_t shard_bytes = 0;     // host bytes per extra GPU before a batch is sharded
+  std::mutex timing_mu;
+  double last_wall_ms = 0, last_kernel_ms = 0;
+};
+
 Runtime& rt() {
   static Runtime* r = new Runtime;  // intentionally leaked: no teardown order issues
   return *r;
 }
 
+Dev& primary() { return *rt().devs[0]; }
+
 std::once_flag g_init_once;
+
+// Devices to bind: QSMD5_DEVICES = "all" or a comma list of ordinals (an
+// ordinal may repeat: two contexts on one GPU, used by the tests to exercise
+// sharding on a one-GPU box); otherwise the single QSMD5_DEVICE / current one.
+int parse_devices(int n, std::vector<int>* out) {
+  const char* ev = getenv("QSMD5_DEVICES");
+  if (ev && *ev) {
+    if (!strcmp(ev, "all")) {
+      for (int d = 0; d < n; ++d) out->push_back(d);
+      return 0;
+    }
+    const char* p = ev;
+    while (*p) {
+      char* end = nullptr;
+      long d = strtol(p, &end, 10);
+      if (end == p) return fail(-EINVAL, "qsmd5: QSMD5_DEVICES is not a comma list of ordinals");
+      if (d < 0 || d >= n) return fail(-ENODEV, "qsmd5: QSMD5_DEVICES names a missing GPU");
+      out->push_back((int)d);
+      p = end;
+      if (*p == ',') ++p;
+      else if (*p) return fail(-EINVAL, "qsmd5: QSMD5_DEVICES is not a comma list of ordinals");
+    }
+    if (out->empty() || out->size() > 64) return fail(-EINVAL, "qsmd5: QSMD5_DEVICES needs 1..64 ordinals");
+    return 0;
+  }
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  const char* ed = getenv("QSMD5_DEVICE");
+  if (ed && *ed) dev = atoi(ed);
+  if (dev < 0 || dev >= n) return fail(-ENODEV, "qsmd5: QSMD5_DEVICE out of range");
+  out->push_back(dev);
+  return 0;
+}
+
+int init_dev(Dev& d, int device) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  d.device = device;
+  d.ncopy = (int)std::min<uint64_t>(kMaxCopyStreams,
+                                     std::max<uint64_t>(1, env_u64("QSMD5_COPY_STREAMS", 2)));
+  for (int k = 0; k < d.ncopy; ++k)
+    if ((e = hipStreamCreateWithFlags(&d.copy[k], hipStreamNonBlocking)) != hipSuccess)
+      return hip_fail(e, "hipStreamCreate");
+  for (auto& s : d.compute)
+    if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
+      return hip_fail(e, "hipStreamCreate");
+  d.staging_cap = env_u64("QSMD5_STAGING_BYTES", kDefaultStaging);
+  return 0;
+}
 
 void do_init() {
   Runtime& r = rt();
@@ -165,34 +226,21 @@ void do_init() {
     r.init_rc = fail(-ENODEV, "qsmd5: no usable GPU (hipGetDeviceCount)");
     return;
   }
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
-  const char* ed = getenv("QSMD5_DEVICE");
-  if (ed && *ed) dev = atoi(ed);
-  if (dev < 0 || dev >= n) {
-    r.init_rc = fail(-ENODEV, "qsmd5: QSMD5_DEVICE out of range");
+  std::vector<int> ords;
+  if (int rc = parse_devices(n, &ords)) {
+    r.init_rc = rc;
     return;
   }
-  if ((e = hipSetDevice(dev)) != hipSuccess) {
-    r.init_rc = hip_fail(e, "hipSetDevice");
-    return;
-  }
-  r.ncopy = (int)std::min<uint64_t>(kMaxCopyStreams,
-                                     std::max<uint64_t>(1, env_u64("QSMD5_COPY_STREAMS", 2)));
-  for (int k = 0; k < r.ncopy; ++k) {
-    if ((e = hipStreamCreateWithFlags(&r.copy[k], hipStreamNonBlocking)) != hipSuccess) {
-      r.init_rc = hip_fail(e, "hipStreamCreate");
-      return;
+  for (int o : ords) {
+    Dev* d = new Dev;
+    if (int rc = init_dev(*d, o)) {
+      r.init_rc = rc;
+      return;  // partially built Devs are leaked with the runtime: init failed for good
     }
+    r.devs.push_back(d);
   }
-  for (auto& s : r.compute) {
-    if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) {
-      r.init_rc = hip_fail(e, "hipStreamCreate");
-      return;
-    }
-  }
-  r.staging_cap = env_u64("QSMD5_STAGING_BYTES", kDefaultStaging);
-  r.device = dev;
+  r.shard_bytes = env_u64("QSMD5_SHARD_BYTES", 4ull << 30);
+  (void)hipSetDevice(r.devs[0]->device);
   r.ready = true;
   r.init_rc = 0;
 }
@@ -203,8 +251,8 @@ int ensure_init() {
   if (!r.ready) return r.init_rc ? r.init_rc : -ENODEV;
   // Calls may come from threads whose current device differs.
   int cur = -1;
-  if (hipGetDevice(&cur) != hipSuccess || cur != r.device) {
-    hipError_t e = hipSetDevice(r.device);
+  if (hipGetDevice(&cur) != hipSuccess || cur != r.devs[0]->device) {
+    hipError_t e = hipSetDevice(r.devs[0]->device);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
   }
   return 0;
@@ -212,7 +260,9 @@ int ensure_init() {
 
 enum MemKind { kHostMem = 0, kDeviceMem = 1 };
 
-MemKind classify(const void* p) {
+// Device memory reports its GPU ordinal in *owner (host memory: -1).
+MemKind classify(const void* p, int* owner = nullptr) {
+  if (owner) *owner = -1;
   if (!p) return kHostMem;
   hipPointerAttribute_t a;
   memset(&a, 0, sizeof(a));
@@ -221,7 +271,9 @@ MemKind classify(const void* p) {
     (void)hipGetLastError();  // pageable host memory: clear the sticky error
     return kHostMem;
   }
-  return a.type == hipMemoryTypeDevice ? kDeviceMem : kHostMem;
+  if (a.type != hipMemoryTypeDevice) return kHostMem;
+  if (owner) *owner = a.device;
+  return kDeviceMem;
 }
 
 int kernel_choice(size_t n, bool aligned16) {
@@ -261,10 +313,11 @@ constexpr uint64_t kColGrain = 64ull << 10;  // automatic column widths are mult
 constexpr uint64_t kColMin = 1ull << 20;     // ... and at least this (>= 1 MiB per-chunk copies)
 constexpr uint64_t kNoColumns = ~0ull;
 
-// The synchronous batch: device chunks in one launch; host chunks staged in
-// slices with copy/compute overlap.  Caller holds rt().mu.
-int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
-  Runtime& r = rt();
+// The synchronous batch on one GPU: device chunks in one launch; host chunks
+// staged in slices with copy/compute overlap.  Caller holds r.mu and has made
+// r.device current.  Device chunks must live on r.device: a kernel reading
+// another GPU's memory would fault unless peer access happens to be enabled.
+int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
   auto t0 = std::chrono::steady_clock::now();
   if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
 
@@ -277,7 +330,11 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
     if (L >= kMaxChunkLen) return fail(-EINVAL, "qsmd5: chunk longer than 2^38 bytes");
     if (L > 0 && !chunks[i].ptr) return fail(-EINVAL, "qsmd5: NULL ptr with non-zero len");
     len[i] = L;
-    kind[i] = L ? classify(chunks[i].ptr) : kDeviceMem;  // empty chunks read nothing
+    int owner = -1;
+    kind[i] = L ? classify(chunks[i].ptr, &owner) : kDeviceMem;  // empty chunks read nothing
+    if (L && kind[i] == kDeviceMem && owner != r.device)
+      return fail(-EINVAL, "qsmd5: chunk lives on GPU " + std::to_string(owner) +
+                               ", not on a bound GPU (QSMD5_DEVICE/QSMD5_DEVICES)");
     if (kind[i] == kHostMem) {
       max_host = std::max(max_host, L);
       host_total += stage_bytes(L);
@@ -546,6 +603,109 @@ int run_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   return 0;
 }
 
+// Multi-GPU batch (QSMD5_DEVICES binds more than one GPU).
+// Device chunks run on the GPU that holds them.  Host chunks (the qsfs case)
+// are cut into contiguous, byte-balanced ranges over k = min(#GPUs,
+// ceil(host bytes / QSMD5_SHARD_BYTES)) GPUs: host data is bound by each GPU's
+// own PCIe link, so shards add ingest bandwidth, while a small batch stays on
+// one GPU (a chain costs ~85 ms per 10 MiB on any number of GPUs).  One thread
+// per GPU runs run_batch on its shard, and the digests are scattered back by
+// chunk index.  In one process there is no collective: every shard's digests
+// land in host memory.  (One process per GPU is qsmd5/parallel.py: RCCL.)
+int run_sharded(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags,
+                double* kernel_ms, double* wall_ms) {
+  Runtime& R = rt();
+  auto t0 = std::chrono::steady_clock::now();
+  const size_t nd = R.devs.size();
+  std::vector<std::vector<uint32_t>> part(nd);
+  std::vector<uint32_t> host;
+  uint64_t host_bytes = 0;
+  if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t L = chunks[i].len;
+    if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;
+    int owner = -1;
+    if (L && chunks[i].ptr && classify(chunks[i].ptr, &owner) == kDeviceMem) {
+      size_t d = 0;
+      while (d < nd && R.devs[d]->device != owner) ++d;
+      if (d == nd)
+        return fail(-EINVAL, "qsmd5: chunk lives on GPU " + std::to_string(owner) +
+                                 ", not on a bound GPU (QSMD5_DEVICES)");
+      part[d].push_back((uint32_t)i);
+    } else {
+      host.push_back((uint32_t)i);
+      host_bytes += L;
+    }
+  }
+  const uint64_t per = std::max<uint64_t>(1, R.shard_bytes);
+  const size_t k = (size_t)std::min<uint64_t>(nd, std::max<uint64_t>(1, (host_bytes + per - 1) / per));
+  uint64_t cum = 0;
+  size_t sh = 0;
+  for (uint32_t i : host) {
+    uint64_t L = chunks[i].len;
+    if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;
+    // shard sh takes chunks while the bytes before them are below its share
+    while (sh + 1 < k && cum >= host_bytes / k * (sh + 1)) ++sh;
+    part[sh].push_back(i);
+    cum += L;
+  }
+  if (env_u64("QSMD5_TRACE", 0)) {
+    for (size_t d = 0; d < nd; ++d)
+      fprintf(stderr, "qsmd5 shard: context %zu (GPU %d) takes %zu chunks\n", d, R.devs[d]->device,
+              part[d].size());
+  }
+  std::vector<int> rc(nd, 0);
+  std::vector<std::string> err(nd);
+  std::vector<double> kms(nd, 0.0);
+  auto work = [&](size_t d) {
+    try {
+      const std::vector<uint32_t>& idx = part[d];
+      std::vector<qsmd5_chunk> sub(idx.size());
+      for (size_t j = 0; j < idx.size(); ++j) sub[j] = chunks[idx[j]];
+      std::vector<uint8_t> dig(16 * idx.size());
+      Dev& dv = *R.devs[d];
+      hipError_t e = hipSetDevice(dv.device);
+      if (e != hipSuccess) {
+        rc[d] = hip_fail(e, "hipSetDevice");
+      } else {
+        std::lock_guard<std::mutex> lk(dv.mu);
+        rc[d] = run_batch(dv, sub.data(), sub.size(), reinterpret_cast<uint8_t(*)[16]>(dig.data()),
+                          flags);
+        kms[d] = dv.last_kernel_ms;
+      }
+      if (rc[d] == 0)
+        for (size_t j = 0; j < idx.size(); ++j) memcpy(digests[idx[j]], &dig[16 * j], 16);
+    } catch (const std::bad_alloc&) {
+      rc[d] = fail(-ENOMEM, "qsmd5: host allocation failed");
+    } catch (...) {
+      rc[d] = fail(-EIO, "qsmd5: internal error");
+    }
+    if (rc[d]) err[d] = t_last_error;  // thread_local: carry it to the caller
+  };
+  std::vector<std::thread> th;
+  size_t mine = nd;
+  for (size_t d = 0; d < nd; ++d) {
+    if (part[d].empty()) continue;
+    if (mine == nd) {
+      mine = d;  // the calling thread takes the first shard
+      continue;
+    }
+    try {
+      th.emplace_back(work, d);
+    } catch (...) {
+      work(d);  // no thread available: run it here
+    }
+  }
+  if (mine != nd) work(mine);
+  for (auto& t : th) t.join();
+  (void)hipSetDevice(R.devs[0]->device);
+  for (size_t d = 0; d < nd; ++d)
+    if (rc[d]) return fail(rc[d], err[d]);
+  *kernel_ms = *std::max_element(kms.begin(), kms.end());
+  *wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return 0;
+}
+
 template <class F>
 int guarded(F&& f) {
   try {
@@ -638,8 +798,24 @@ int qsmd5_hash_batch_ex(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[
     if (n == 0) return 0;
     if (!chunks || !digests) return fail(-EINVAL, "qsmd5: NULL chunks/digests");
     if (int rc = ensure_init()) return rc;
-    std::lock_guard<std::mutex> lk(rt().mu);
-    return run_batch(chunks, n, digests, flags);
+    Runtime& R = rt();
+    int rc = 0;
+    double kernel_ms = 0, wall_ms = 0;
+    if (R.devs.size() == 1) {
+      Dev& d = primary();
+      std::lock_guard<std::mutex> lk(d.mu);
+      rc = run_batch(d, chunks, n, digests, flags);
+      kernel_ms = d.last_kernel_ms;
+      wall_ms = d.last_wall_ms;
+    } else {
+      rc = run_sharded(chunks, n, digests, flags, &kernel_ms, &wall_ms);
+    }
+    if (rc == 0) {
+      std::lock_guard<std::mutex> lk(R.timing_mu);
+      R.last_kernel_ms = kernel_ms;
+      R.last_wall_ms = wall_ms;
+    }
+    return rc;
   });
 }
 
@@ -788,7 +964,7 @@ int qsmd5_verify_etag(const void* ptr, uint64_t len, const char* etag) {
 
 int qsmd5_last_timing(double* wall_ms, double* kernel_ms) {
   Runtime& r = rt();
-  std::lock_guard<std::mutex> lk(r.mu);
+  std::lock_guard<std::mutex> lk(r.timing_mu);
   if (wall_ms) *wall_ms = r.last_wall_ms;
   if (kernel_ms) *kernel_ms = r.last_kernel_ms;
   return 0;
@@ -836,7 +1012,7 @@ void qsmd5_ctx_destroy(qsmd5_ctx* c) {
 }
 
 static int ctx_blocks(qsmd5_ctx* c, const uint8_t* p, uint64_t nblk, bool on_device) {
-  Runtime& r = rt();
+  Dev& r = primary();
   hipStream_t s = r.compute[0];
   const uint8_t* src = p;
   if (!on_device) {
@@ -868,8 +1044,12 @@ int qsmd5_ctx_update(qsmd5_ctx* c, const void* ptr, uint64_t len) {
     if (len == 0) return 0;
     if (!ptr) return fail(-EINVAL, "qsmd5: NULL ptr with non-zero len");
     if (int rc = ensure_init()) return rc;
-    std::lock_guard<std::mutex> lk(rt().mu);
-    const bool dev = classify(ptr) == kDeviceMem;
+    std::lock_guard<std::mutex> lk(primary().mu);
+    int owner = -1;
+    const bool dev = classify(ptr, &owner) == kDeviceMem;
+    if (dev && owner != primary().device)
+      return fail(-EINVAL, "qsmd5: update data lives on GPU " + std::to_string(owner) +
+                               ", not on the primary bound GPU");
     const uint8_t* p = static_cast<const uint8_t*>(ptr);
     uint64_t left = len;
     c->total += len;
@@ -911,8 +1091,8 @@ int qsmd5_ctx_final(qsmd5_ctx* c, uint8_t digest[16]) {
     if (!c || !digest) return fail(-EINVAL, "qsmd5: NULL ctx/digest");
     if (!c->finalized) {
       if (int rc = ensure_init()) return rc;
-      std::lock_guard<std::mutex> lk(rt().mu);
-      hipStream_t s = rt().compute[0];
+      std::lock_guard<std::mutex> lk(primary().mu);
+      hipStream_t s = primary().compute[0];
       QS_HIP(hipMemcpyAsync(c->d_tail, c->tail, 64, hipMemcpyHostToDevice, s));
       QS_HIP(qsmd5::launch_final(c->d_state, c->d_tail, c->tail_len, c->total, s));
       QS_HIP(hipMemcpyAsync(c->digest, c->d_state, 16, hipMemcpyDeviceToHost, s));
