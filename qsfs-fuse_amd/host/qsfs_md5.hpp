@@ -7,6 +7,9 @@
 //   std::string md5(const shared_ptr<std::iostream>&)  MD5.h:96, MD5.cpp:341-349
 //   class MD5 { update; finalize; hexdigest; << }      MD5.h:51-93
 //
+// plus the batch forms the reference lacks: md5_batch() and md5_file_parts()
+// (all parts of a file in one GPU pass).
+//
 // md5(stream) hashes exactly the bytes the reference hashes -- from position 0
 // to the end of the stream's get area, i.e. the first lengthToRead bytes of a
 // qsfs StreamBuf (StreamBuf.cpp:32-48) -- and, like the reference, leaves the
@@ -113,6 +116,50 @@ std::string md5(const StreamPtr& stream) {
   }
   stream->clear();
   stream->seekg(0, std::ios_base::beg);
+  return out;
+}
+
+// Batch form: the hex MD5 of every buffer, in order,
+// from ONE qsmd5_hash_batch call -- one GPU pass for all parts of a file
+// instead of one md5(buffer) per part (File.cpp:641,644 hash them serially).
+inline std::vector<std::string> md5_batch(const std::vector<qsmd5_chunk>& chunks) {
+  std::vector<std::string> out;
+  if (chunks.empty()) return out;
+  std::vector<uint8_t> dig(16 * chunks.size());
+  detail::check(qsmd5_hash_batch(chunks.data(), chunks.size(),
+                                 reinterpret_cast<uint8_t(*)[16]>(dig.data())),
+                "qsmd5_hash_batch");
+  out.reserve(chunks.size());
+  for (size_t i = 0; i < chunks.size(); ++i) out.push_back(detail::hex(&dig[16 * i]));
+  return out;
+}
+
+// One upload part and its Content-MD5 text.
+struct PartMD5 {
+  qsmd5_part part;  // number, offset, size as QSTransferManager::PrepareUpload slices
+  std::string md5;  // what UploadMultipart would pass to SetContentMD5 (QSClient.cpp:370)
+};
+
+// Every part of a file held in one buffer, sliced exactly as PrepareUpload
+// does (QSTransferManager.cpp:475-550: single PutObject below `threshold`,
+// else `buf_size` parts with the short tail averaged into the previous part
+// when it is below `min_part`), hashed in one batch.  Defaults are qsfs's:
+// -b 10 MiB buffers, 4 MiB minimum part, 20 MiB multipart threshold.
+inline std::vector<PartMD5> md5_file_parts(const void* file, uint64_t size,
+                                           uint64_t buf_size = 10ull << 20,
+                                           uint64_t min_part = 4ull << 20,
+                                           uint64_t threshold = 20ull << 20) {
+  size_t n = 0;
+  detail::check(qsmd5_plan_parts(size, buf_size, min_part, threshold, 0, nullptr, 0, &n),
+                "qsmd5_plan_parts");
+  std::vector<qsmd5_part> parts(n);
+  detail::check(qsmd5_plan_parts(size, buf_size, min_part, threshold, 0, parts.data(), n, &n),
+                "qsmd5_plan_parts");
+  std::vector<uint8_t> dig(16 * n);
+  detail::check(qsmd5_hash_parts(file, parts.data(), n, reinterpret_cast<uint8_t(*)[16]>(dig.data())),
+                "qsmd5_hash_parts");
+  std::vector<PartMD5> out(n);
+  for (size_t i = 0; i < n; ++i) out[i] = PartMD5{parts[i], detail::hex(&dig[16 * i])};
   return out;
 }
 

@@ -123,7 +123,37 @@ int main() {
     qsmd5::MD5 one(std::string("abc"));
     std::printf("class_ctor_abc %s\n", one.hexdigest().c_str());
   }
-  // 5. Errors are loud: NULL pointer with a non-zero length.
+  // 5. Batch forms: md5_batch over ragged buffers, md5_file_parts over a
+  //    25 MiB + 3 B "file" (PrepareUpload: 10, 10, 5 MiB + 3 B) and a 21 MiB one
+  //    (10 MiB, then the 11 MiB remainder averaged into two 5.5 MiB parts).
+  {
+    std::vector<std::vector<char>> bufs;
+    std::vector<qsmd5_chunk> chunks;
+    for (size_t i = 0; i < 6; ++i) bufs.push_back(lcg(500 + (uint32_t)i, 1000 * i * i + 3 * i));
+    for (auto& b : bufs) chunks.push_back(qsmd5_chunk{b.data(), b.size()});
+    std::vector<std::string> hx = qsmd5::md5_batch(chunks);
+    expect(hx.size() == bufs.size(), "md5_batch returns one digest per buffer");
+    for (size_t i = 0; i < hx.size(); ++i) {
+      std::printf("batch_%zu %s\n", i, hx[i].c_str());
+      expect(hx[i] == qsmd5::md5_bytes(bufs[i].data(), bufs[i].size()), "md5_batch == md5_bytes");
+    }
+    for (uint64_t fsz : {uint64_t(25) * 1048576 + 3, uint64_t(21) * 1048576}) {
+      std::vector<char> file = lcg(777, fsz);
+      std::vector<qsmd5::PartMD5> parts = qsmd5::md5_file_parts(file.data(), file.size());
+      uint64_t covered = 0;
+      for (const auto& pm : parts) {
+        std::printf("parts_%llu_%u %llu %llu %s\n", (unsigned long long)fsz, pm.part.part_number,
+                    (unsigned long long)pm.part.offset, (unsigned long long)pm.part.size,
+                    pm.md5.c_str());
+        expect(pm.part.offset == covered, "parts are contiguous");
+        expect(pm.md5 == qsmd5::md5_bytes(file.data() + pm.part.offset, pm.part.size),
+               "md5_file_parts == md5 of the part bytes");
+        covered += pm.part.size;
+      }
+      expect(covered == fsz, "parts cover the file");
+    }
+  }
+  // 6. Errors are loud: NULL pointer with a non-zero length.
   {
     bool threw = false;
     try {

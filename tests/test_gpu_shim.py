@@ -35,7 +35,7 @@ def test_cpp_dropin_shim():
         build_shim()
     out = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
-    got = dict(line.split() for line in out.stdout.strip().splitlines())
+    got = dict(line.split() for line in out.stdout.strip().splitlines() if not line.startswith("parts_"))
     h = lambda b: hashlib.md5(b).hexdigest()
     assert got["str_empty"] == h(b"")
     assert got["str_abc"] == h(b"abc")
@@ -48,4 +48,16 @@ def test_cpp_dropin_shim():
     assert got["stringstream_100000q"] == h(b"q" * 100000)
     assert got["class_pieces"] == h(bytes(lcg_bytes(4242, 200000)))
     assert got["class_ctor_abc"] == h(b"abc")
+    for i in range(6):
+        assert got["batch_%d" % i] == h(bytes(lcg_bytes(500 + i, 1000 * i * i + 3 * i + 1))[:1000 * i * i + 3 * i])
+    MiB = 1 << 20
+    rows = [l.split() for l in out.stdout.splitlines() if l.startswith("parts_")]
+    for fsz, sizes in ((25 * MiB + 3, [10 * MiB, 10 * MiB, 5 * MiB + 3]),
+                       (21 * MiB, [10 * MiB, 11 * MiB // 2, 11 * MiB - 11 * MiB // 2])):
+        mine = [r for r in rows if r[0].startswith("parts_%d_" % fsz)]
+        assert [int(r[2]) for r in mine] == sizes, mine
+        data = bytes(lcg_bytes(777, fsz))
+        for r in mine:
+            off, sz = int(r[1]), int(r[2])
+            assert r[3] == h(data[off:off + sz]), r
     assert got["failures"] == "0"
