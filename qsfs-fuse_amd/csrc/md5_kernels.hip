@@ -251,7 +251,7 @@ __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*rin
 #pragma unroll
   for (int h = 0; h < kPcHalf; ++h) {
     if (h + 1 < kPcHalf) read_slot((h & 1) ? a : b, s0 + h + 1);
-    if (kAllLive || blk0 + h < nblk) compress_slot((h & 1) ? b : a);
+    if (kAllLive || blk0 + (uint32_t)h < nblk) compress_slot((h & 1) ? b : a);  // blk0 may wrap (skew)
   }
 }
 
@@ -372,11 +372,23 @@ extern "C" __global__ __launch_bounds__(256) void qsmd5_lcg_fill_kernel(
 // and then either parks the state (L - col_off > col_w) or finishes with the
 // tail and the full length L (MD5.cpp:279-312 over the whole message).
 // col_off and col_w are multiples of 64, so block boundaries line up.
-template <bool kColumn>
+//
+// skew (whole-chunk batches only; a multiple of kPcHalf): in a wave whose
+// longest chunk has >= kSkewMinBlocks blocks (32 MiB), lane l starts its chain
+// perm(l) x skew blocks late, so the 64 lanes read addresses spread over up to
+// 63 x skew x 64 B instead of the same offset of every chunk at once.  Long
+// parts at a power-of-two stride (a contiguous device file cut into 32 or
+// 64 MiB parts, qsfs -b 32/64) otherwise send every lane's request to the same
+// HBM channels: measured 512 x 64 MiB 42.1 -> 54.5 GiB/s, 512 x 32 MiB
+// 48.6 -> 54.7 (profiles/r01_ubench_skew.log).  Cost: 63 x skew blocks per
+// wave (0.05% of a 32 MiB chain); shorter chunks never pay it.  0 = off.
+constexpr uint32_t kSkewMinBlocks = 1u << 19;
+template <bool kColumn, int kDepth = 1>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
                                         uint32_t* __restrict__ digests, uint64_t col_off,
-                                        uint64_t col_w, uint32_t* __restrict__ states) {
+                                        uint64_t col_w, uint32_t* __restrict__ states,
+                                        uint32_t skew) {
   __shared__ u32x4 ring[kPcSlots][16][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
@@ -399,7 +411,12 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     }
   }
   const uint32_t nblk = (uint32_t)(seg >> 6);
-  const uint32_t phases = (wave_max_u32(nblk) + kPcHalf - 1) / kPcHalf;
+  // start delay in blocks; lanes take the delays in a scrambled order (37 is odd,
+  // so l -> 37 l mod 64 is a permutation) so that no affine chunk stride can
+  // cancel the spread
+  const bool skewed = !kColumn && skew != 0 && wave_max_u32(nblk) >= kSkewMinBlocks;
+  const uint32_t delta = (skewed && nblk) ? skew * ((lane * 37u) & 63u) : 0u;
+  const uint32_t phases = (wave_max_u32(nblk + delta) + kPcHalf - 1) / kPcHalf;
   const uintptr_t pa = reinterpret_cast<uintptr_t>(cd.ptr);
   const uint32_t off = (uint32_t)(pa & 3u);
 
@@ -407,32 +424,47 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     // ---------------- producer ----------------
     const uint32_t* base = reinterpret_cast<const uint32_t*>(pa & ~uintptr_t(3));
     const uint32_t last = nblk ? nblk - 1 : 0;
-    PcBlockRegs r[kPcHalf];
-    auto load_phase = [&](uint32_t p) {
+    // kDepth register sets of one phase each: the loads of phase q go into set
+    // q % kDepth and are written to the ring kDepth phases after they were
+    // issued, so a load has kDepth phases (~2 us each) to land.
+    PcBlockRegs r[kDepth][kPcHalf];
+    auto load_phase = [&](PcBlockRegs (&rs)[kPcHalf], uint32_t p) {
       if (nblk) {
 #pragma unroll
-        for (int h = 0; h < kPcHalf; ++h) pc_load_block(r[h], base, off, min(p * kPcHalf + h, last));
+        for (int h = 0; h < kPcHalf; ++h) {
+          const uint32_t j = p * kPcHalf + h;  // virtual block; the lane's block is j - delta
+          pc_load_block(rs[h], base, off, j < delta ? 0u : min(j - delta, last));
+        }
       }
     };
-    auto write_phase = [&](uint32_t p) {
+    auto write_phase = [&](const PcBlockRegs (&rs)[kPcHalf], uint32_t p) {
       if (nblk) {
 #pragma unroll
         for (int h = 0; h < kPcHalf; ++h)
-          pc_write_mk(ring[(p & 1u) * kPcHalf + h], lane, r[h], off);
+          pc_write_mk(ring[(p & 1u) * kPcHalf + h], lane, rs[h], off);
       }
     };
     if (phases > 0) {
-      load_phase(0);
-      write_phase(0);
-      load_phase(1);
+#pragma unroll
+      for (int k = 0; k < kDepth; ++k) load_phase(r[k], (uint32_t)k);
+      write_phase(r[0], 0);
+      load_phase(r[0], kDepth);
     }
     lds_barrier();
-    for (uint32_t p = 0; p < phases; ++p) {
-      if (p + 1 < phases) {
-        write_phase(p + 1);
-        load_phase(p + 2);
+    // iteration p writes phase p + 1 from set (p + 1) % kDepth and refills that
+    // set with phase p + 1 + kDepth; unrolled by kDepth so every set is static
+    for (uint32_t p0 = 0; p0 < phases; p0 += kDepth) {
+#pragma unroll
+      for (int u = 0; u < kDepth; ++u) {
+        const uint32_t p = p0 + (uint32_t)u;
+        if (p < phases) {
+          if (p + 1 < phases) {
+            write_phase(r[(u + 1) % kDepth], p + 1);
+            load_phase(r[(u + 1) % kDepth], p + 1 + kDepth);
+          }
+          lds_barrier();
+        }
       }
-      lds_barrier();
     }
     return;
   }
@@ -440,7 +472,8 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
   // ---------------- chain ----------------
   // Phases in which every live lane still has all kPcHalf blocks run without a
   // per-block lane predicate (wave-uniform branch on an SGPR).
-  const uint32_t live_phases = rfl_u32(wave_min_u32(t < n ? nblk : 0xffffffffu) / kPcHalf);
+  const uint32_t live_lo = rfl_u32((wave_max_u32(delta) + kPcHalf - 1) / kPcHalf);
+  const uint32_t live_hi = rfl_u32(wave_min_u32(t < n ? nblk + delta : 0xffffffffu) / kPcHalf);
   uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
   if (kColumn && col_off != 0 && t < n) {
     const u32x4 s4 = *reinterpret_cast<const u32x4*>(states + 4u * (uint64_t)idx);
@@ -452,10 +485,10 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
   lds_barrier();
   for (uint32_t p = 0; p < phases; ++p) {
     const uint32_t s0 = (p & 1u) * kPcHalf;
-    if (p < live_phases)
-      chain_phase<true>(st, ring, s0, lane, p * kPcHalf, nblk);
+    if (p >= live_lo && p < live_hi)
+      chain_phase<true>(st, ring, s0, lane, p * kPcHalf - delta, nblk);
     else
-      chain_phase<false>(st, ring, s0, lane, p * kPcHalf, nblk);
+      chain_phase<false>(st, ring, s0, lane, p * kPcHalf - delta, nblk);
     lds_barrier();
   }
   if (t >= n) return;
@@ -471,15 +504,15 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
 
 extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
-    uint32_t* __restrict__ digests) {
-  pc_body<false>(chunks, order, n, digests, 0, ~0ull, nullptr);
+    uint32_t* __restrict__ digests, uint32_t skew) {
+  pc_body<false>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
 }
 
 extern "C" __global__ __launch_bounds__(128) void qsmd5_column_pc_kernel(
     const ChunkDesc* __restrict__ segs, const uint32_t* __restrict__ order, uint32_t n,
     uint32_t* __restrict__ digests, uint64_t col_off, uint64_t col_w,
     uint32_t* __restrict__ states) {
-  pc_body<true>(segs, order, n, digests, col_off, col_w, states);
+  pc_body<true>(segs, order, n, digests, col_off, col_w, states, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -662,12 +695,13 @@ extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_coal_kernel(
 namespace qsmd5 {
 
 hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
-                        int kind, hipStream_t s) {
+                        int kind, hipStream_t s, uint32_t skew_blocks) {
   if (n == 0) return hipSuccess;
   const uint32_t groups = (n + 63u) / 64u;
   if (kind == kKernelLatency) {
     hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(groups), dim3(128), 0, s,
-                       static_cast<const ChunkDesc*>(chunks), order, n, digests);
+                       static_cast<const ChunkDesc*>(chunks), order, n, digests,
+                       skew_blocks / kPcHalf * kPcHalf);
   } else if (kind == kKernelCoalesced) {
     hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3(groups), dim3(64), 0, s,
                        static_cast<const ChunkDesc*>(chunks), order, n, digests);

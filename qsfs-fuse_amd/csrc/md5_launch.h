@@ -19,8 +19,13 @@ constexpr uint32_t kLatencyKernelResident = 256u * 64u;
 
 // chunks: device array of {ptr,len}; order: optional device lane->chunk map;
 // digests: device, 16 B per chunk indexed by chunk index.
+// Start skew of the latency kernel for waves whose longest chunk is >= 32 MiB
+// (see pc_body): lane l starts perm(l) x skew blocks late.
+constexpr uint32_t kPcSkewBlocks = 4;
+
+// skew_blocks: latency kernel only (rounded down to a multiple of 4; 0 = off).
 hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
-                        int kind, hipStream_t s);
+                        int kind, hipStream_t s, uint32_t skew_blocks = kPcSkewBlocks);
 // Column-pipelined latency kernel: lane t hashes segment segs[t] = {staged
 // start of bytes [col_off, col_off + col_w) of chunk order[t], that chunk's
 // total length}; state parks in states[4 * order[t]] between columns and the

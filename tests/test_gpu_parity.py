@@ -133,6 +133,28 @@ def test_bufsize_sweep_device(golden):
         assert hexes(got) == sw["md5"], sw["mib"]
 
 
+def test_start_skew_wave_mixed_lengths():
+    """A wave whose longest chunk is >= 32 MiB runs with per-lane start skew
+    (pc_body): lanes with tiny, empty, unaligned and multi-block chunks in the
+    same wave must still hash exactly their own bytes."""
+    big = 32 * MiB + 77
+    lens = [big, 32 * MiB, 0, 1, 55, 56, 63, 64, 65, 127, 128, 1000, 4096 + 3, 65536 + 9,
+            3 * MiB + 1] + [1 + 97 * i for i in range(40)]
+    offs, pos = [], 0
+    for i, L in enumerate(lens):
+        pos += 1 + (i % 7)  # unaligned starts
+        offs.append(pos)
+        pos += L
+    t = torch.empty(pos + 256, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    qsmd5.synth_fill_lcg(t.data_ptr(), 0, pos + 256, 31337, 1, s)
+    torch.cuda.synchronize()
+    raw = t.cpu().numpy()
+    want = md5_many([(raw.ctypes.data + o, L) for o, L in zip(offs, lens)])
+    got = qsmd5.hash_batch([(t.data_ptr() + o, L) for o, L in zip(offs, lens)])
+    assert got == want
+
+
 def _device_batch(n, L, seed0):
     t = dev_lcg(seed0, L, nchunks=n)
     desc = torch.empty((n, 2), dtype=torch.int64)

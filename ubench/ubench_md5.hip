@@ -32,6 +32,14 @@ extern "C" {
     }                                                                              \
   } while (0)
 
+// Latency kernel with a deeper producer prefetch (kDepth phases of loads in flight).
+template <int D>
+__global__ __launch_bounds__(128) void k_pc_depth(const ChunkDesc* __restrict__ c,
+                                                  const uint32_t* __restrict__ o, uint32_t n,
+                                                  uint32_t* __restrict__ d, uint32_t skew) {
+  pc_body<false, D>(c, o, n, d, 0, ~0ull, nullptr, skew);
+}
+
 // ---- 1. issue / latency ----------------------------------------------------
 #define REP8(x) x x x x x x x x
 #define REP64(x) REP8(REP8(x))
@@ -171,6 +179,7 @@ static double run_issue(ukern k, int instr_per_iter, int iters, int threads) {
 
 // ---- 2. MD5 batch kernel -----------------------------------------------------
 static bool g_host_pinned = false;  // "zc" mode: chunks in pinned host memory (zero-copy)
+static uint32_t g_skew = kPcSkewBlocks;  // latency kernel start skew (blocks per lane)
 
 static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint64_t pad = 0) {
   uint64_t stride = ((L + 255) & ~uint64_t(255)) + pad;
@@ -203,10 +212,16 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
                          (uint32_t)B, d_dig);
     else if (which == 1)
       hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
-                         (uint32_t)B, d_dig);
-    else
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 2)
       hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3(grid), dim3(64), 0, 0, d_desc, nullptr,
                          (uint32_t)B, d_dig);
+    else if (which == 3)
+      hipLaunchKernelGGL(k_pc_depth<2>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else
+      hipLaunchKernelGGL(k_pc_depth<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
   };
   launch();
   CK(hipGetLastError());
@@ -226,10 +241,11 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   med = s[s.size() / 2];
   double gib = (double)L * B / (1u << 30);
   if (pad) printf("(stride pad %llu) ", (unsigned long long)pad);
+  if (which != 0 && which != 2 && g_skew) printf("(skew %u) ", g_skew);
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : "coal", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -293,10 +309,16 @@ static int run_edges(int which) {
                        (uint32_t)n, dg);
   else if (which == 1)
     hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
-                       (uint32_t)n, dg);
-  else
+                       (uint32_t)n, dg, g_skew);
+  else if (which == 2)
     hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, dd, nullptr,
                        (uint32_t)n, dg);
+  else if (which == 3)
+    hipLaunchKernelGGL(k_pc_depth<2>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
+                       (uint32_t)n, dg, g_skew);
+  else
+    hipLaunchKernelGGL(k_pc_depth<3>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
+                       (uint32_t)n, dg, g_skew);
   CK(hipDeviceSynchronize());
   std::vector<uint8_t> got(16 * n);
   CK(hipMemcpy(got.data(), dg, 16 * n, hipMemcpyDeviceToHost));
@@ -703,6 +725,18 @@ int main(int argc, char** argv) {
     run_md5(512, 32ull << 20, 2, false, 0, 0);
     run_md5(512, 32ull << 20, 2, false, 0, 4096);
     return 0;
+  }
+  if (!strcmp(mode, "skew")) {
+    // latency kernel on long strided chunks: start skew x producer prefetch depth
+    int bad = 0;
+    for (int w : {1, 3, 4}) {
+      bad += run_edges(w);
+      for (uint64_t mib : {10ull, 32ull, 64ull}) run_md5(512, mib << 20, 2, mib == 64, w, 0);
+      for (uint64_t mib : {32ull, 64ull}) run_md5(512, mib << 20, 2, false, w, 4096);
+      run_md5(512, 64ull << 20, 2, false, w, 65536 + 256);
+      run_md5(100, (32ull << 20) + 64 * 7 + 13, 2, true, w, 0);  // ragged tail, partial wave
+    }
+    return bad ? 1 : 0;
   }
   if (!strcmp(mode, "cross")) {
     // latency (pc) vs coalesced kernel around the selection threshold (16384 chunks)
