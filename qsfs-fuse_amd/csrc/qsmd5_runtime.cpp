@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <new>
 #include <numeric>
@@ -706,6 +707,138 @@ int run_sharded(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
   return 0;
 }
 
+// ---- group commit ------------------------------------------------------------
+// qsfs hashes parts from up to numtransfer executor threads at once
+// (TransferManager.cpp:55-60) plus FUSE threads, each call a batch of its own
+// (often one part).  A batch costs one chain time (~85 ms per 10 MiB) whatever
+// its width, so concurrent calls are merged: a caller that finds the GPU idle
+// becomes the leader and runs every queued request as ONE batch; callers that
+// arrive meanwhile queue and are taken by the next leader.  Five concurrent
+// one-part calls then cost two chain times instead of five.  A merged batch
+// that fails (one caller's bad pointer, an allocation too large for the merged
+// size) is re-run request by request, so each caller gets its own result.
+struct Request {
+  const qsmd5_chunk* chunks;
+  size_t n;
+  uint8_t (*digests)[16];
+  int flags;
+  int rc = 0;
+  std::string err;
+  bool done = false;
+};
+
+struct Coalescer {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Request*> queue;
+  bool busy = false;
+};
+
+Coalescer& coalescer() {
+  static Coalescer* c = new Coalescer;  // leaked, as rt()
+  return *c;
+}
+
+constexpr size_t kMaxGroupChunks = 1u << 24;
+
+// One batch on the bound GPU(s); timings go to the runtime's last_* fields.
+int run_any(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
+  Runtime& R = rt();
+  int rc = 0;
+  double kernel_ms = 0, wall_ms = 0;
+  if (R.devs.size() == 1) {
+    Dev& d = primary();
+    std::lock_guard<std::mutex> lk(d.mu);
+    rc = run_batch(d, chunks, n, digests, flags);
+    kernel_ms = d.last_kernel_ms;
+    wall_ms = d.last_wall_ms;
+  } else {
+    rc = run_sharded(chunks, n, digests, flags, &kernel_ms, &wall_ms);
+  }
+  if (rc == 0) {
+    std::lock_guard<std::mutex> lk(R.timing_mu);
+    R.last_kernel_ms = kernel_ms;
+    R.last_wall_ms = wall_ms;
+  }
+  return rc;
+}
+
+void run_group(const std::vector<Request*>& group) {
+  // Nothing may escape: the leader must always clear `busy` (see group_commit).
+  auto run_one = [](Request* q) {
+    try {
+      q->rc = run_any(q->chunks, q->n, q->digests, q->flags);
+    } catch (const std::bad_alloc&) {
+      q->rc = fail(-ENOMEM, "qsmd5: host allocation failed");
+    } catch (...) {
+      q->rc = fail(-EIO, "qsmd5: internal error");
+    }
+    if (q->rc) q->err = t_last_error;
+  };
+  if (group.size() == 1) {
+    run_one(group[0]);
+    return;
+  }
+  size_t total = 0;
+  for (Request* q : group) total += q->n;
+  std::vector<qsmd5_chunk> merged;
+  std::vector<uint8_t> dig;
+  int rc = 0;
+  try {
+    merged.reserve(total);
+    for (Request* q : group)
+      for (size_t i = 0; i < q->n; ++i) {
+        qsmd5_chunk c = q->chunks[i];
+        if (q->flags & QSMD5_FLAG_REF_TRUNCATE32) c.len &= 0xffffffffull;  // per caller
+        merged.push_back(c);
+      }
+    dig.resize(16 * total);
+    rc = run_any(merged.data(), total, reinterpret_cast<uint8_t(*)[16]>(dig.data()), 0);
+  } catch (...) {
+    rc = -ENOMEM;  // re-run one by one below
+  }
+  if (rc != 0) {
+    for (Request* q : group) run_one(q);  // each caller gets its own result
+    return;
+  }
+  size_t off = 0;
+  for (Request* q : group) {
+    memcpy(q->digests, &dig[16 * off], 16 * q->n);
+    off += q->n;
+  }
+}
+
+int group_commit(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
+  if (env_u64("QSMD5_NO_COALESCE", 0)) return run_any(chunks, n, digests, flags);
+  Coalescer& co = coalescer();
+  Request req{chunks, n, digests, flags};
+  std::unique_lock<std::mutex> lk(co.mu);
+  co.queue.push_back(&req);
+  while (!req.done) {
+    if (co.busy) {
+      co.cv.wait(lk);
+      continue;
+    }
+    // Lead: take queued requests (FIFO) up to kMaxGroupChunks, at least one.
+    co.busy = true;
+    std::vector<Request*> group;
+    size_t total = 0, k = 0;
+    while (k < co.queue.size() && (group.empty() || total + co.queue[k]->n <= kMaxGroupChunks)) {
+      total += co.queue[k]->n;
+      group.push_back(co.queue[k++]);
+    }
+    co.queue.erase(co.queue.begin(), co.queue.begin() + k);
+    lk.unlock();
+    run_group(group);
+    lk.lock();
+    for (Request* q : group) q->done = true;
+    co.busy = false;
+    co.cv.notify_all();
+  }
+  if (req.rc) t_last_error = req.err;  // the leader's thread ran it
+  return req.rc;
+}
+
 template <class F>
 int guarded(F&& f) {
   try {
@@ -797,25 +930,9 @@ int qsmd5_hash_batch_ex(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[
   return guarded([&] {
     if (n == 0) return 0;
     if (!chunks || !digests) return fail(-EINVAL, "qsmd5: NULL chunks/digests");
+    if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
     if (int rc = ensure_init()) return rc;
-    Runtime& R = rt();
-    int rc = 0;
-    double kernel_ms = 0, wall_ms = 0;
-    if (R.devs.size() == 1) {
-      Dev& d = primary();
-      std::lock_guard<std::mutex> lk(d.mu);
-      rc = run_batch(d, chunks, n, digests, flags);
-      kernel_ms = d.last_kernel_ms;
-      wall_ms = d.last_wall_ms;
-    } else {
-      rc = run_sharded(chunks, n, digests, flags, &kernel_ms, &wall_ms);
-    }
-    if (rc == 0) {
-      std::lock_guard<std::mutex> lk(R.timing_mu);
-      R.last_kernel_ms = kernel_ms;
-      R.last_wall_ms = wall_ms;
-    }
-    return rc;
+    return group_commit(chunks, n, digests, flags);
   });
 }
 
