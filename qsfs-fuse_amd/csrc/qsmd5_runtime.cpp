@@ -725,12 +725,14 @@ struct Request {
   int rc = 0;
   std::string err;
   bool done = false;
+  Request* next = nullptr;  // intrusive FIFO: queueing and taking never allocate
 };
 
 struct Coalescer {
   std::mutex mu;
   std::condition_variable cv;
-  std::vector<Request*> queue;
+  Request* head = nullptr;
+  Request* tail = nullptr;
   bool busy = false;
 };
 
@@ -763,49 +765,57 @@ int run_any(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int fla
   return rc;
 }
 
-void run_group(const std::vector<Request*>& group) {
-  // Nothing may escape: the leader must always clear `busy` (see group_commit).
+// Runs the requests first, first->next, ... (nothing may escape: the leader
+// must always get back to clearing `busy` in group_commit).
+void run_group(Request* first) noexcept {
   auto run_one = [](Request* q) {
+    const char* what = nullptr;
     try {
       q->rc = run_any(q->chunks, q->n, q->digests, q->flags);
     } catch (const std::bad_alloc&) {
-      q->rc = fail(-ENOMEM, "qsmd5: host allocation failed");
+      q->rc = -ENOMEM;
+      what = "qsmd5: host allocation failed";
     } catch (...) {
-      q->rc = fail(-EIO, "qsmd5: internal error");
+      q->rc = -EIO;
+      what = "qsmd5: internal error";
     }
-    if (q->rc) q->err = t_last_error;
+    if (q->rc) {
+      try {
+        q->err = what ? std::string(what) : t_last_error;
+      } catch (...) {
+      }
+    }
   };
-  if (group.size() == 1) {
-    run_one(group[0]);
+  if (!first->next) {
+    run_one(first);
     return;
   }
-  size_t total = 0;
-  for (Request* q : group) total += q->n;
-  std::vector<qsmd5_chunk> merged;
-  std::vector<uint8_t> dig;
   int rc = 0;
   try {
+    size_t total = 0;
+    for (Request* q = first; q; q = q->next) total += q->n;
+    std::vector<qsmd5_chunk> merged;
     merged.reserve(total);
-    for (Request* q : group)
+    for (Request* q = first; q; q = q->next)
       for (size_t i = 0; i < q->n; ++i) {
         qsmd5_chunk c = q->chunks[i];
         if (q->flags & QSMD5_FLAG_REF_TRUNCATE32) c.len &= 0xffffffffull;  // per caller
         merged.push_back(c);
       }
-    dig.resize(16 * total);
+    std::vector<uint8_t> dig(16 * total);
     rc = run_any(merged.data(), total, reinterpret_cast<uint8_t(*)[16]>(dig.data()), 0);
+    if (rc == 0) {
+      size_t off = 0;
+      for (Request* q = first; q; q = q->next) {
+        memcpy(q->digests, &dig[16 * off], 16 * q->n);
+        off += q->n;
+      }
+      return;
+    }
   } catch (...) {
-    rc = -ENOMEM;  // re-run one by one below
+    // fall through: re-run one by one
   }
-  if (rc != 0) {
-    for (Request* q : group) run_one(q);  // each caller gets its own result
-    return;
-  }
-  size_t off = 0;
-  for (Request* q : group) {
-    memcpy(q->digests, &dig[16 * off], 16 * q->n);
-    off += q->n;
-  }
+  for (Request* q = first; q; q = q->next) run_one(q);  // each caller gets its own result
 }
 
 int group_commit(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
@@ -813,25 +823,35 @@ int group_commit(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], in
   Coalescer& co = coalescer();
   Request req{chunks, n, digests, flags};
   std::unique_lock<std::mutex> lk(co.mu);
-  co.queue.push_back(&req);
+  if (co.tail) co.tail->next = &req;
+  else co.head = &req;
+  co.tail = &req;
   while (!req.done) {
     if (co.busy) {
       co.cv.wait(lk);
       continue;
     }
-    // Lead: take queued requests (FIFO) up to kMaxGroupChunks, at least one.
+    // Lead: take the queue's head requests (FIFO) up to kMaxGroupChunks, at least one.
     co.busy = true;
-    std::vector<Request*> group;
-    size_t total = 0, k = 0;
-    while (k < co.queue.size() && (group.empty() || total + co.queue[k]->n <= kMaxGroupChunks)) {
-      total += co.queue[k]->n;
-      group.push_back(co.queue[k++]);
+    Request* first = co.head;
+    Request* last = first;
+    size_t total = first->n;
+    while (last->next && total + last->next->n <= kMaxGroupChunks) {
+      last = last->next;
+      total += last->n;
     }
-    co.queue.erase(co.queue.begin(), co.queue.begin() + k);
+    co.head = last->next;
+    if (!co.head) co.tail = nullptr;
+    last->next = nullptr;
     lk.unlock();
-    run_group(group);
+    run_group(first);
     lk.lock();
-    for (Request* q : group) q->done = true;
+    // Waiters read `done` only under the lock, so a request stays alive here.
+    for (Request* q = first; q;) {
+      Request* nx = q->next;
+      q->done = true;
+      q = nx;
+    }
     co.busy = false;
     co.cv.notify_all();
   }
