@@ -112,6 +112,38 @@ def config3(reps, n=4096, label=""):
         qsmd5.free_pinned(p)
 
 
+def config3_pageable(reps, n=1024):
+    """Config 3's flow from ordinary pageable host memory: what qsfs has today,
+    its ResourceManager buffers being plain vector<char> (ResourceManager.cpp:53-77),
+    not the pinned pool of SURVEY.md §8f row 2."""
+    import numpy as np
+    import torch
+    import qsmd5
+    L = 10 * MiB
+    g = gold("batch_10MiB.json")["md5"][:n]
+    host = np.empty(n * L, dtype=np.uint8)
+    step = 256
+    buf = torch.empty(step * L, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for k in range(0, n, step):
+        m = min(step, n - k)
+        qsmd5.synth_fill_lcg(buf.data_ptr(), L, L, 12345 + k, m, s)
+        torch.from_numpy(host[k * L:(k + m) * L]).copy_(buf[:m * L])
+    torch.cuda.synchronize()
+    del buf
+    base = host.ctypes.data
+    chunks = [(base + i * L, L) for i in range(n)]
+    dt, digs = timed(lambda: qsmd5.hash_batch(chunks), reps)
+    wall, kern = qsmd5.last_timing()
+    ok = [d.hex() for d in digs] == g
+    emit({"config": "3-pageable", "workload": "%d x 10 MiB in PAGEABLE host memory, end-to-end "
+                                              "(H2D + hash + D2H digests)" % n,
+          "value": round(n * L / GiB / dt, 3), "unit": "GiB/s", "seconds": round(dt, 4),
+          "last_call_wall_ms": round(wall, 2), "last_call_kernel_window_ms": round(kern, 2),
+          "parity": "ok: %d/%d == reference golden" % (n, n) if ok else "FAIL"})
+    del host
+
+
 def config4(reps):
     import torch
     import qsmd5
@@ -230,6 +262,8 @@ def main():
             config1()
         elif c == "3":
             config3(args.reps)
+        elif c == "3p":
+            config3_pageable(args.reps)
         elif c == "4":
             config4(args.reps)
         elif c == "5":
