@@ -726,6 +726,14 @@ int main(int argc, char** argv) {
     run_md5(512, 32ull << 20, 2, false, 0, 4096);
     return 0;
   }
+  if (!strcmp(mode, "tlb")) {
+    // 2 MiB-page aliasing test: pads that move each chunk to another 2 MiB page index
+    for (uint64_t mib : {32ull, 64ull})
+      for (uint64_t pad : {0ull, 4096ull, 1ull << 20, 2ull << 20, (2ull << 20) + 4096, 6ull << 20})
+        run_md5(512, mib << 20, 2, false, 1, pad);
+    run_md5(512, 10ull << 20, 2, false, 1, 0);
+    return 0;
+  }
   if (!strcmp(mode, "skew")) {
     // latency kernel on long strided chunks: start skew x producer prefetch depth
     int bad = 0;
