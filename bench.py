@@ -180,8 +180,9 @@ def main():
     desc = desc.to(dev)
     dig = torch.zeros((B, 16), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    kernel = "producer/consumer (qsmd5_batch_pc_kernel)" if qsmd5.kernel_choice(B) == 1 else \
-        "one-wave (qsmd5_batch_kernel)"
+    kernel = {0: "one-wave (qsmd5_batch_kernel)", 1: "producer/consumer (qsmd5_batch_pc_kernel)",
+              2: "coalesced (qsmd5_batch_coal_kernel)",
+              3: "producer/consumer, 64 KiB ring (qsmd5_batch_pc2_kernel)"}[qsmd5.kernel_choice(B)]
 
     def step(ev=None):
         if ev is not None:

@@ -238,7 +238,7 @@ def saturation(reps, L=64 * 1024):
     ok = [bytes(r) for r in dig[:64].cpu().numpy()] == want
     gbs = n * L / (med * 1e-3) / 1e9
     emit({"config": "saturation", "workload": "%d x %d KiB device-resident, stride +4352 B (kernel %s)" % (
-        n, L // 1024, ["v1", "pc", "coal"][qsmd5.kernel_choice(n, qsmd5.FLAG_ALIGNED16)]),
+        n, L // 1024, ["v1", "pc", "coal", "pc2"][qsmd5.kernel_choice(n, qsmd5.FLAG_ALIGNED16)]),
         "GiBps": round(n * L / GiB / (med * 1e-3), 1), "GBps": round(gbs, 1),
         "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "kernel_ms_median": round(med, 3),
         "kernel_ms_best": round(best, 3), "launches": reps,

@@ -124,16 +124,18 @@ QSMD5_API int qsmd5_hash_batch_device_async(const qsmd5_chunk* d_chunks, const u
                                   uint8_t (*d_digests)[16], void* hip_stream);
 
 /* As qsmd5_hash_batch_device_async; flags may carry QSMD5_FLAG_ALIGNED16,
- * which lets batches beyond one resident round (> 16 384 chunks) use the
- * coalesced LDS-DMA throughput kernel. */
+ * which lets batches beyond the latency kernels' range (> 32 768 chunks) use
+ * the coalesced LDS-DMA throughput kernel. */
 QSMD5_API int qsmd5_hash_batch_device_async_ex(const qsmd5_chunk* d_chunks, const uint32_t* d_order,
                                      size_t n, uint8_t (*d_digests)[16], void* hip_stream,
                                      int flags);
 
 /* Which kernel a device batch of n chunks gets: 1 = producer/consumer latency
- * kernel (n <= 16 384), 2 = coalesced throughput kernel (larger, 16-B-aligned
- * chunks), 0 = one-wave throughput kernel (larger, any alignment).
- * QSMD5_KERNEL env ("pc"/"coal"/"v1") overrides. */
+ * kernel, 128 KiB LDS ring, one workgroup per CU (n <= 16 384); 3 = the same
+ * with a 64 KiB ring, two workgroups per CU (n <= 32 768); 2 = coalesced
+ * throughput kernel (larger, 16-B-aligned chunks); 0 = one-wave throughput
+ * kernel (larger, any alignment).  QSMD5_KERNEL env ("pc"/"pc2"/"coal"/"v1")
+ * overrides. */
 QSMD5_API int qsmd5_kernel_choice(size_t n);
 QSMD5_API int qsmd5_kernel_choice_ex(size_t n, int flags);
 

@@ -7,6 +7,8 @@
 //                            BASELINE config): producer wave streams blocks and
 //                            precomputes x[g]+K into LDS, chain wave runs only
 //                            the serial 4-VALU steps.
+//   qsmd5_batch_pc2_kernel   the same with a 64 KiB ring (two workgroups per
+//                            CU): <= 2 x 256 x 64 chunks.
 //   qsmd5_batch_coal_kernel  throughput kernel, more chunks, 16-B aligned:
 //                            coalesced LDS-DMA staging of 128 B per chain.
 //   qsmd5_batch_kernel       throughput kernel, more chunks, any alignment:
@@ -186,8 +188,7 @@ __device__ __forceinline__ void lds_barrier() {
 // for all 64 steps of each block into an LDS ring; wave 0 (chain) runs only the
 // serial part: 4 VALU per step plus one ds_read_b128 per 4 steps.  The two waves
 // sit on different SIMDs, so the chain wave's issue slots are not shared.
-constexpr int kPcHalf = 4;                   // blocks per ring half (one phase)
-constexpr int kPcSlots = 2 * kPcHalf;        // 8 x 16 KiB = 128 KiB of LDS
+constexpr int kPcHalf = 4;  // blocks per ring half (one phase): 8 x 16 KiB = 128 KiB of LDS
 
 struct PcBlockRegs {
   u32x4 q[4];
@@ -227,7 +228,7 @@ __device__ __forceinline__ void pc_write_mk(u32x4 (*slot)[64], uint32_t lane, co
 // One phase of the chain wave: kPcHalf blocks from ring slots s0.., the
 // operands of block h+1 read from LDS while block h compresses.  kAllLive
 // drops the per-block lane predicate (every lane has blocks blk0..blk0+H-1).
-template <bool kAllLive>
+template <bool kAllLive, int kHalf = kPcHalf>
 __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*ring)[16][64],
                                             uint32_t s0, uint32_t lane, uint32_t blk0,
                                             uint32_t nblk) {
@@ -249,8 +250,8 @@ __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*rin
   };
   read_slot(a, s0);
 #pragma unroll
-  for (int h = 0; h < kPcHalf; ++h) {
-    if (h + 1 < kPcHalf) read_slot((h & 1) ? a : b, s0 + h + 1);
+  for (int h = 0; h < kHalf; ++h) {
+    if (h + 1 < kHalf) read_slot((h & 1) ? a : b, s0 + h + 1);
     if (kAllLive || blk0 + (uint32_t)h < nblk) compress_slot((h & 1) ? b : a);  // blk0 may wrap (skew)
   }
 }
@@ -383,13 +384,13 @@ extern "C" __global__ __launch_bounds__(256) void qsmd5_lcg_fill_kernel(
 // 48.6 -> 54.7 (profiles/r01_ubench_skew.log).  Cost: 63 x skew blocks per
 // wave (0.05% of a 32 MiB chain); shorter chunks never pay it.  0 = off.
 constexpr uint32_t kSkewMinBlocks = 1u << 19;
-template <bool kColumn, int kDepth = 1>
+template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
                                         uint32_t* __restrict__ digests, uint64_t col_off,
                                         uint64_t col_w, uint32_t* __restrict__ states,
                                         uint32_t skew) {
-  __shared__ u32x4 ring[kPcSlots][16][64];
+  __shared__ u32x4 ring[2 * kHalf][16][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t t = blockIdx.x * 64u + lane;
@@ -416,7 +417,7 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
   // cancel the spread
   const bool skewed = !kColumn && skew != 0 && wave_max_u32(nblk) >= kSkewMinBlocks;
   const uint32_t delta = (skewed && nblk) ? skew * ((lane * 37u) & 63u) : 0u;
-  const uint32_t phases = (wave_max_u32(nblk + delta) + kPcHalf - 1) / kPcHalf;
+  const uint32_t phases = (wave_max_u32(nblk + delta) + kHalf - 1) / kHalf;
   const uintptr_t pa = reinterpret_cast<uintptr_t>(cd.ptr);
   const uint32_t off = (uint32_t)(pa & 3u);
 
@@ -427,21 +428,21 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     // kDepth register sets of one phase each: the loads of phase q go into set
     // q % kDepth and are written to the ring kDepth phases after they were
     // issued, so a load has kDepth phases (~2 us each) to land.
-    PcBlockRegs r[kDepth][kPcHalf];
-    auto load_phase = [&](PcBlockRegs (&rs)[kPcHalf], uint32_t p) {
+    PcBlockRegs r[kDepth][kHalf];
+    auto load_phase = [&](PcBlockRegs (&rs)[kHalf], uint32_t p) {
       if (nblk) {
 #pragma unroll
-        for (int h = 0; h < kPcHalf; ++h) {
-          const uint32_t j = p * kPcHalf + h;  // virtual block; the lane's block is j - delta
+        for (int h = 0; h < kHalf; ++h) {
+          const uint32_t j = p * kHalf + h;  // virtual block; the lane's block is j - delta
           pc_load_block(rs[h], base, off, j < delta ? 0u : min(j - delta, last));
         }
       }
     };
-    auto write_phase = [&](const PcBlockRegs (&rs)[kPcHalf], uint32_t p) {
+    auto write_phase = [&](const PcBlockRegs (&rs)[kHalf], uint32_t p) {
       if (nblk) {
 #pragma unroll
-        for (int h = 0; h < kPcHalf; ++h)
-          pc_write_mk(ring[(p & 1u) * kPcHalf + h], lane, rs[h], off);
+        for (int h = 0; h < kHalf; ++h)
+          pc_write_mk(ring[(p & 1u) * kHalf + h], lane, rs[h], off);
       }
     };
     if (phases > 0) {
@@ -470,10 +471,10 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
   }
 
   // ---------------- chain ----------------
-  // Phases in which every live lane still has all kPcHalf blocks run without a
+  // Phases in which every live lane still has all kHalf blocks run without a
   // per-block lane predicate (wave-uniform branch on an SGPR).
-  const uint32_t live_lo = rfl_u32((wave_max_u32(delta) + kPcHalf - 1) / kPcHalf);
-  const uint32_t live_hi = rfl_u32(wave_min_u32(t < n ? nblk + delta : 0xffffffffu) / kPcHalf);
+  const uint32_t live_lo = rfl_u32((wave_max_u32(delta) + kHalf - 1) / kHalf);
+  const uint32_t live_hi = rfl_u32(wave_min_u32(t < n ? nblk + delta : 0xffffffffu) / kHalf);
   uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
   if (kColumn && col_off != 0 && t < n) {
     const u32x4 s4 = *reinterpret_cast<const u32x4*>(states + 4u * (uint64_t)idx);
@@ -484,11 +485,11 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
   }
   lds_barrier();
   for (uint32_t p = 0; p < phases; ++p) {
-    const uint32_t s0 = (p & 1u) * kPcHalf;
+    const uint32_t s0 = (p & 1u) * kHalf;
     if (p >= live_lo && p < live_hi)
-      chain_phase<true>(st, ring, s0, lane, p * kPcHalf - delta, nblk);
+      chain_phase<true, kHalf>(st, ring, s0, lane, p * kHalf - delta, nblk);
     else
-      chain_phase<false>(st, ring, s0, lane, p * kPcHalf - delta, nblk);
+      chain_phase<false, kHalf>(st, ring, s0, lane, p * kHalf - delta, nblk);
     lds_barrier();
   }
   if (t >= n) return;
@@ -508,11 +509,26 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
   pc_body<false>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
 }
 
+// 2-block phases: a 64 KiB ring, so two workgroups (four waves) share a CU and
+// one launch keeps 2 x 256 x 64 chunks resident (kKernelLatency2).
+extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc2_kernel(
+    const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
+    uint32_t* __restrict__ digests, uint32_t skew) {
+  pc_body<false, 1, 2>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
+}
+
 extern "C" __global__ __launch_bounds__(128) void qsmd5_column_pc_kernel(
     const ChunkDesc* __restrict__ segs, const uint32_t* __restrict__ order, uint32_t n,
     uint32_t* __restrict__ digests, uint64_t col_off, uint64_t col_w,
     uint32_t* __restrict__ states) {
   pc_body<true>(segs, order, n, digests, col_off, col_w, states, 0u);
+}
+
+extern "C" __global__ __launch_bounds__(128) void qsmd5_column_pc2_kernel(
+    const ChunkDesc* __restrict__ segs, const uint32_t* __restrict__ order, uint32_t n,
+    uint32_t* __restrict__ digests, uint64_t col_off, uint64_t col_w,
+    uint32_t* __restrict__ states) {
+  pc_body<true, 1, 2>(segs, order, n, digests, col_off, col_w, states, 0u);
 }
 
 // ---------------------------------------------------------------------------
@@ -702,6 +718,10 @@ hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, u
     hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(groups), dim3(128), 0, s,
                        static_cast<const ChunkDesc*>(chunks), order, n, digests,
                        skew_blocks / kPcHalf * kPcHalf);
+  } else if (kind == kKernelLatency2) {
+    hipLaunchKernelGGL(qsmd5_batch_pc2_kernel, dim3(groups), dim3(128), 0, s,
+                       static_cast<const ChunkDesc*>(chunks), order, n, digests,
+                       skew_blocks / kPcHalf * kPcHalf);
   } else if (kind == kKernelCoalesced) {
     hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3(groups), dim3(64), 0, s,
                        static_cast<const ChunkDesc*>(chunks), order, n, digests);
@@ -715,9 +735,14 @@ hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, u
 hipError_t launch_column(const void* segs, const uint32_t* order, uint32_t n, uint32_t* digests,
                          uint64_t col_off, uint64_t col_w, uint32_t* states, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(qsmd5_column_pc_kernel, dim3((n + 63u) / 64u), dim3(128), 0, s,
-                     static_cast<const ChunkDesc*>(segs), order, n, digests, col_off, col_w,
-                     states);
+  if (n > kLatencyKernelResident)  // beyond one resident round: two workgroups per CU
+    hipLaunchKernelGGL(qsmd5_column_pc2_kernel, dim3((n + 63u) / 64u), dim3(128), 0, s,
+                       static_cast<const ChunkDesc*>(segs), order, n, digests, col_off, col_w,
+                       states);
+  else
+    hipLaunchKernelGGL(qsmd5_column_pc_kernel, dim3((n + 63u) / 64u), dim3(128), 0, s,
+                       static_cast<const ChunkDesc*>(segs), order, n, digests, col_off, col_w,
+                       states);
   return hipGetLastError();
 }
 

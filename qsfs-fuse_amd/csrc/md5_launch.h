@@ -11,11 +11,14 @@ enum KernelKind : int {
   kKernelThroughput = 0,  // qsmd5_batch_kernel: 1 wave / 64 chunks, all work in-wave
   kKernelLatency = 1,     // qsmd5_batch_pc_kernel: producer + chain wave / 64 chunks
   kKernelCoalesced = 2,   // qsmd5_batch_coal_kernel: LDS-DMA coalesced staging, 16-B-aligned
+  kKernelLatency2 = 3,    // qsmd5_batch_pc2_kernel: the latency kernel with a 64 KiB ring
 };
 
 // Chunks one launch of the latency kernel keeps resident at once: one
-// 128 KiB-LDS workgroup per CU, 64 chunks each.
+// 128 KiB-LDS workgroup per CU, 64 chunks each.  The 64 KiB-ring variant fits
+// two workgroups per CU (2-block phases: ~3% slower per chain, measured).
 constexpr uint32_t kLatencyKernelResident = 256u * 64u;
+constexpr uint32_t kLatency2KernelResident = 2u * 256u * 64u;
 
 // chunks: device array of {ptr,len}; order: optional device lane->chunk map;
 // digests: device, 16 B per chunk indexed by chunk index.

@@ -40,6 +40,7 @@ namespace {
 
 using qsmd5::kKernelCoalesced;
 using qsmd5::kKernelLatency;
+using qsmd5::kKernelLatency2;
 using qsmd5::kKernelThroughput;
 
 constexpr uint64_t kMaxChunkLen = 1ull << 38;
@@ -280,13 +281,18 @@ MemKind classify(const void* p, int* owner = nullptr) {
 int kernel_choice(size_t n, bool aligned16) {
   const char* k = getenv("QSMD5_KERNEL");
   if (k && !strcmp(k, "pc")) return kKernelLatency;
+  if (k && !strcmp(k, "pc2")) return kKernelLatency2;
   if (k && !strcmp(k, "v1")) return kKernelThroughput;
   if (k && !strcmp(k, "coal")) return aligned16 ? kKernelCoalesced : kKernelThroughput;
   // The latency kernel wins while every chunk has its own chain lane in one
-  // resident round (one 128 KiB-LDS workgroup per CU); beyond that the
-  // throughput kernels keep 2+ waves per SIMD and the bound moves to HBM,
-  // where coalesced LDS-DMA staging beats per-lane loads (16-B-aligned chunks).
+  // resident round (one 128 KiB-LDS workgroup per CU); its 64 KiB-ring variant
+  // doubles the round (two workgroups per CU) at ~3% per chain, which still
+  // beats the throughput kernels up to 32 768 chunks (+16% at 20-24 K, +6% at
+  // 32 K; profiles/r01_ubench_cross2.log).  Beyond that the throughput kernels
+  // keep 2+ waves per SIMD and the bound moves to VALU x clock and HBM, where
+  // coalesced LDS-DMA staging beats per-lane loads (16-B-aligned chunks).
   if (n <= qsmd5::kLatencyKernelResident) return kKernelLatency;
+  if (n <= qsmd5::kLatency2KernelResident) return kKernelLatency2;
   return aligned16 ? kKernelCoalesced : kKernelThroughput;
 }
 

@@ -179,3 +179,17 @@ def test_config3_pinned_4096_columns(golden, columns):
         assert hexes(got) == g["md5"][:n]
     finally:
         qsmd5.free_pinned(p)
+
+
+def test_columns_beyond_one_resident_round(columns):
+    """A host batch of > 16 384 chunks cut into columns runs the column kernel
+    with the 64 KiB ring (two workgroups per CU, qsmd5_column_pc2_kernel)."""
+    import random
+    rng = random.Random(17)
+    n = 18000
+    data = lcg_bytes(99, 2 * MiB)
+    base = ctypes.addressof(data)
+    spans = [(rng.randrange(0, MiB), rng.randrange(0, 3000)) for _ in range(n)]
+    want = md5_many([(base + o, L) for o, L in spans])
+    columns(1024)
+    assert qsmd5.hash_batch([(base + o, L) for o, L in spans]) == want

@@ -32,7 +32,7 @@ def _gpu():
     os.environ.pop("QSMD5_KERNEL", None)
 
 
-@pytest.fixture(params=["pc", "v1", "coal"])
+@pytest.fixture(params=["pc", "pc2", "v1", "coal"])
 def kernel(request):
     os.environ["QSMD5_KERNEL"] = request.param
     yield request.param
@@ -292,8 +292,10 @@ def test_kernel_choice_policy():
     A = qsmd5.FLAG_ALIGNED16
     assert qsmd5.kernel_choice(512) == 1 and qsmd5.kernel_choice(512, A) == 1
     assert qsmd5.kernel_choice(16384) == 1
-    assert qsmd5.kernel_choice(16385) == 0
-    assert qsmd5.kernel_choice(16385, A) == 2
+    assert qsmd5.kernel_choice(16385) == 3 and qsmd5.kernel_choice(16385, A) == 3
+    assert qsmd5.kernel_choice(32768) == 3
+    assert qsmd5.kernel_choice(32769) == 0
+    assert qsmd5.kernel_choice(32769, A) == 2
 
 
 def test_coalesced_kernel_ragged_aligned(kernel):
@@ -314,10 +316,12 @@ def test_coalesced_kernel_ragged_aligned(kernel):
     assert got == want
 
 
-def test_coalesced_kernel_device_async_large():
-    """> 16 384 chunks with QSMD5_FLAG_ALIGNED16 goes to the coalesced kernel."""
+@pytest.mark.parametrize("n,kind", [(20000, 3), (40000, 2)])
+def test_device_async_large_batches(n, kind):
+    """16 385..32 768 chunks go to the 64 KiB-ring latency kernel, more (with
+    QSMD5_FLAG_ALIGNED16) to the coalesced kernel."""
     os.environ.pop("QSMD5_KERNEL", None)
-    n, L = 20000, 4096 + 64 + 7
+    L = 4096 + 64 + 7
     S = 8192 + 16
     t = dev_lcg(3, L, nchunks=n, stride=S)
     desc = torch.empty((n, 2), dtype=torch.int64)
@@ -325,7 +329,7 @@ def test_coalesced_kernel_device_async_large():
     desc[:, 1] = L
     desc = desc.cuda()
     dig = torch.zeros((n, 16), dtype=torch.uint8, device="cuda")
-    assert qsmd5.kernel_choice(n, qsmd5.FLAG_ALIGNED16) == 2
+    assert qsmd5.kernel_choice(n, qsmd5.FLAG_ALIGNED16) == kind
     qsmd5.hash_device(desc.data_ptr(), dig.data_ptr(), n,
                       stream=torch.cuda.current_stream().cuda_stream, flags=qsmd5.FLAG_ALIGNED16)
     torch.cuda.synchronize()
@@ -348,13 +352,14 @@ def test_verify_etag_download_buffer():
         qsmd5.verify_etag(data, etag[:-2] + '-2"')
 
 
-def test_large_batches_select_throughput_kernels():
-    """> 16 384 chunks through the synchronous API: staged host chunks (aligned ->
-    coalesced kernel) and unaligned device chunks (one-wave kernel)."""
+@pytest.mark.parametrize("n", [17000, 33000])
+def test_large_batches_select_throughput_kernels(n):
+    """> 16 384 chunks through the synchronous API: staged host chunks and
+    unaligned device chunks (17 000: 64 KiB-ring latency kernel; 33 000:
+    coalesced kernel for the staged chunks, one-wave kernel for the unaligned)."""
     os.environ.pop("QSMD5_KERNEL", None)
     import random
     rng = random.Random(8)
-    n = 17000
     host = lcg_bytes(71, 4 << 20)
     base = ctypes.addressof(host)
     spans = [(rng.randrange(0, (4 << 20) - 5000), rng.randrange(0, 5000)) for _ in range(n)]

@@ -40,6 +40,13 @@ __global__ __launch_bounds__(128) void k_pc_depth(const ChunkDesc* __restrict__ 
   pc_body<false, D>(c, o, n, d, 0, ~0ull, nullptr, skew);
 }
 
+// Latency kernel with 2-block phases: a 64 KiB LDS ring, two workgroups per CU.
+__global__ __launch_bounds__(128) void k_pc_half2(const ChunkDesc* __restrict__ c,
+                                                  const uint32_t* __restrict__ o, uint32_t n,
+                                                  uint32_t* __restrict__ d, uint32_t skew) {
+  pc_body<false, 1, 2>(c, o, n, d, 0, ~0ull, nullptr, skew);
+}
+
 // ---- 1. issue / latency ----------------------------------------------------
 #define REP8(x) x x x x x x x x
 #define REP64(x) REP8(REP8(x))
@@ -219,6 +226,9 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 3)
       hipLaunchKernelGGL(k_pc_depth<2>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
+    else if (which == 5)
+      hipLaunchKernelGGL(k_pc_half2, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
     else
       hipLaunchKernelGGL(k_pc_depth<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
@@ -245,7 +255,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -315,6 +325,9 @@ static int run_edges(int which) {
                        (uint32_t)n, dg);
   else if (which == 3)
     hipLaunchKernelGGL(k_pc_depth<2>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
+                       (uint32_t)n, dg, g_skew);
+  else if (which == 5)
+    hipLaunchKernelGGL(k_pc_half2, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew);
   else
     hipLaunchKernelGGL(k_pc_depth<3>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
@@ -748,9 +761,11 @@ int main(int argc, char** argv) {
   }
   if (!strcmp(mode, "cross")) {
     // latency (pc) vs coalesced kernel around the selection threshold (16384 chunks)
-    for (int B : {8192, 12288, 16384, 20480, 24576, 32768, 49152})
-      for (int w : {1, 2}) run_md5(B, 1 << 20, 3, false, w, 4352);
-    return 0;
+    int bad = run_edges(5);
+    for (int B : {512, 8192, 16384, 20480, 24576, 32768, 49152})
+      for (int w : {1, 5, 2}) run_md5(B, 1 << 20, 3, w == 5, w, 4352);
+    run_md5(512, 10 << 20, 3, true, 5, 0);
+    return bad ? 1 : 0;
   }
   if (!strcmp(mode, "coalfast")) {
     // A/B: the previous coal body (probe copy, mode 0) vs the shipped kernel with the fast region
