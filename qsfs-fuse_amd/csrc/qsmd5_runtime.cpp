@@ -348,6 +348,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     }
   }
 
+  const auto t_classified = std::chrono::steady_clock::now();
   // Lane order: device chunks first, then host chunks; each group sorted by
   // length (descending) so the lanes of a wavefront finish together.
   std::vector<uint32_t> dev_idx, host_idx;
@@ -356,6 +357,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   std::sort(dev_idx.begin(), dev_idx.end(), by_len);
   std::sort(host_idx.begin(), host_idx.end(), by_len);
 
+  const auto t_sorted = std::chrono::steady_clock::now();
   // Column width: one column of every host chunk should fill about one slice.
   const uint64_t slice_target = env_u64(
       "QSMD5_SLICE_BYTES", std::min(kSliceMax, std::max(kSliceMin, host_total / 4)));
@@ -458,6 +460,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   for (uint32_t ci : dev_idx) ho[pos++] = ci;
   for (uint32_t ci : host_idx) ho[pos++] = ci;
 
+  const auto t_planned = std::chrono::steady_clock::now();
   hipStream_t s0 = r.compute[0];
   EventSet events;
   // On any failure after work was enqueued, wait for it before returning: an
@@ -593,6 +596,13 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   if (e != hipSuccess) return drain(hip_fail(e, "hipStreamSynchronize"));
   memcpy(digests, r.h_dig.p, n * 16);
   if (trace) {
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+      return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t_end = std::chrono::steady_clock::now();
+    fprintf(stderr, "qsmd5 trace: %zu chunks: classify %.2f ms, sort %.2f ms, plan %.2f ms, "
+            "enqueue+run %.2f ms\n", n, ms(t0, t_classified), ms(t_classified, t_sorted),
+            ms(t_sorted, t_planned), ms(t_planned, t_end));
     fprintf(stderr, "qsmd5 trace: %zu slices, column width %llu, %zu groups, %zu regions\n",
             slices.size(), (unsigned long long)(W == kNoColumns ? 0 : W), groups.size(), nregions);
     for (size_t si = 0; si < slices.size(); ++si) {
