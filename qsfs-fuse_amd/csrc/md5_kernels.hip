@@ -549,20 +549,31 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_column_pc2_kernel(
 #define QS_LP(p) ((__attribute__((address_space(3))) void*)(uintptr_t)(uint32_t)(uintptr_t)(p))
 
 // One fast-region tile U of a group (see batch_coal_body): prefetch the next
-// tile from each instruction's source pointer into buffer (U + 1) & 1 and
-// advance the pointer, then compress tile U from buffer U & 1 with no lane
-// predicate.  The DMA immediate offset is NOT usable to step through a chunk:
-// the hardware adds it to the LDS destination as well as to the global address.
-template <int U, int kU, int kTB, int kS, int kCPI>
+// tile into buffer (U + 1) & 1, then compress tile U from buffer U & 1 with no
+// lane predicate.  kImm = false: each DMA source pointer is bumped per tile
+// (1 VALU each).  kImm = true: the pointers stay at the group's first prefetch
+// tile and tile U is reached with the instruction's immediate offset U x 128.
+// The hardware adds that offset to the LDS destination as well as to the
+// global address, so the LDS base passed in (M0) is lowered by the same amount
+// (the caller pads the LDS buffer in front to keep it non-negative).
+template <int U, int kU, int kTB, int kS, int kCPI, bool kImm>
 __device__ __forceinline__ void coal_fast_group(uint32_t (&st)[4], const uint8_t* (&gp)[kS],
                                                 u32x4 (*tile_buf)[64][kS], uint32_t lane,
                                                 uint32_t rswz) {
   if constexpr (U < kU) {
 #pragma unroll
     for (int i = 0; i < kS; ++i) {
-      __builtin_amdgcn_global_load_lds(QS_GP(gp[i]), QS_LP(&tile_buf[(U + 1) & 1][i * kCPI][0]), 16,
-                                       0, 0);
-      gp[i] += kTB * 64;
+      if constexpr (kImm) {
+        constexpr int kOff = U * kTB * 64;
+        __builtin_amdgcn_global_load_lds(
+            QS_GP(gp[i]),
+            QS_LP(reinterpret_cast<uintptr_t>(&tile_buf[(U + 1) & 1][i * kCPI][0]) - kOff), 16,
+            kOff, 0);
+      } else {
+        __builtin_amdgcn_global_load_lds(QS_GP(gp[i]), QS_LP(&tile_buf[(U + 1) & 1][i * kCPI][0]),
+                                         16, 0, 0);
+        gp[i] += kTB * 64;
+      }
     }
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kS) : "memory");
 #pragma unroll
@@ -575,11 +586,11 @@ __device__ __forceinline__ void coal_fast_group(uint32_t (&st)[4], const uint8_t
       md5_compress(st, w);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    coal_fast_group<U + 1, kU, kTB, kS, kCPI>(st, gp, tile_buf, lane, rswz);
+    coal_fast_group<U + 1, kU, kTB, kS, kCPI, kImm>(st, gp, tile_buf, lane, rswz);
   }
 }
 
-template <int kTB, int kBufs>
+template <int kTB, int kBufs, bool kImm = false>
 __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ chunks,
                                                 const uint32_t* __restrict__ order, uint32_t n,
                                                 uint32_t* __restrict__ digests) {
@@ -588,7 +599,11 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
   // one LDS-DMA instruction covers 64 / kS chains, kS instructions per tile.
   constexpr int kS = 4 * kTB;
   constexpr int kCPI = 64 / kS;  // chains per instruction
-  __shared__ u32x4 tile_buf[kBufs][64][kS];
+  // kImm: pad in front of the tiles so that M0 = destination - offset >= 0
+  constexpr int kUImm = 4;
+  constexpr int kPad = kImm ? ((kUImm - 1) * kTB * 64 + 15) / 16 : 0;
+  __shared__ u32x4 tile_raw[kPad + kBufs * 64 * kS];
+  u32x4 (*tile_buf)[64][kS] = reinterpret_cast<u32x4 (*)[64][kS]>(tile_raw + kPad);
   const uint32_t lane = threadIdx.x;
   const uint32_t t = blockIdx.x * 64u + lane;
   uint32_t idx = 0;
@@ -645,15 +660,20 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
     // loop-invariant per-lane addresses.  This removes ~24 VALU per block
     // (352 -> 328, ~7%) in a regime bound by VALU x clock
     // (profiles/r01_ubench_probe.log).
-    constexpr int kU = 2;  // tiles per loop trip: keeps the buffer index static
+    constexpr int kU = kImm ? kUImm : 2;  // tiles per loop trip (even: static buffer index)
     const bool full_wave = (blockIdx.x + 1u) * 64u <= n;
     const uint32_t fast_tiles = full_wave ? rfl_u32(wave_min_u32(nblk)) / (uint32_t)kTB : 0u;
     const uint8_t* gp[kS];  // source of tile tl + 1 for DMA instruction i
 #pragma unroll
     for (int i = 0; i < kS; ++i)
       gp[i] = src[i] + kTB * 64u + (piece[i] >> 2) * 64u + (piece[i] & 3u) * 16u;
-    for (; tl + (uint32_t)kU < fast_tiles; tl += (uint32_t)kU)
-      coal_fast_group<0, kU, kTB, kS, kCPI>(st, gp, tile_buf, lane, rswz);
+    for (; tl + (uint32_t)kU < fast_tiles; tl += (uint32_t)kU) {
+      coal_fast_group<0, kU, kTB, kS, kCPI, kImm>(st, gp, tile_buf, lane, rswz);
+      if constexpr (kImm) {
+#pragma unroll
+        for (int i = 0; i < kS; ++i) gp[i] += kU * kTB * 64;
+      }
+    }
   }
   for (; tl < ntiles; ++tl) {
     const uint32_t b = tl % kBufs;

@@ -47,6 +47,13 @@ __global__ __launch_bounds__(128) void k_pc_half2(const ChunkDesc* __restrict__ 
   pc_body<false, 1, 2>(c, o, n, d, 0, ~0ull, nullptr, skew);
 }
 
+// Coalesced kernel with immediate-offset DMA in the fast region.
+__global__ __launch_bounds__(64) void k_coal_imm(const ChunkDesc* __restrict__ c,
+                                                 const uint32_t* __restrict__ o, uint32_t n,
+                                                 uint32_t* __restrict__ d) {
+  batch_coal_body<2, 2, true>(c, o, n, d);
+}
+
 // ---- 1. issue / latency ----------------------------------------------------
 #define REP8(x) x x x x x x x x
 #define REP64(x) REP8(REP8(x))
@@ -229,6 +236,9 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 5)
       hipLaunchKernelGGL(k_pc_half2, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
+    else if (which == 6)
+      hipLaunchKernelGGL(k_coal_imm, dim3(grid), dim3(64), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig);
     else
       hipLaunchKernelGGL(k_pc_depth<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
@@ -251,11 +261,11 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   med = s[s.size() / 2];
   double gib = (double)L * B / (1u << 30);
   if (pad) printf("(stride pad %llu) ", (unsigned long long)pad);
-  if (which != 0 && which != 2 && g_skew) printf("(skew %u) ", g_skew);
+  if ((which == 1 || which == 3 || which == 4 || which == 5) && g_skew) printf("(skew %u) ", g_skew);
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -329,6 +339,9 @@ static int run_edges(int which) {
   else if (which == 5)
     hipLaunchKernelGGL(k_pc_half2, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew);
+  else if (which == 6)
+    hipLaunchKernelGGL(k_coal_imm, dim3((n + 63) / 64), dim3(64), 0, 0, dd, nullptr, (uint32_t)n,
+                       dg);
   else
     hipLaunchKernelGGL(k_pc_depth<3>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew);
@@ -738,6 +751,18 @@ int main(int argc, char** argv) {
     run_md5(512, 32ull << 20, 2, false, 0, 0);
     run_md5(512, 32ull << 20, 2, false, 0, 4096);
     return 0;
+  }
+  if (!strcmp(mode, "imm")) {
+    // coalesced kernel: per-tile pointer bumps (shipped) vs immediate-offset DMA
+    int bad = run_edges(2) + run_edges(6);
+    for (int rep = 0; rep < 2; ++rep)
+      for (int w : {2, 6}) {
+        run_md5(131072, 65536, 10, rep == 0, w, 4352);
+        run_md5(131072, 262144, 6, rep == 0, w, 4352);
+      }
+    run_md5(100000, 65536 + 17 * 64, 3, true, 6, 4352);
+    run_md5(131072, 65536 + 64 * 3, 3, true, 6, 4352);
+    return bad ? 1 : 0;
   }
   if (!strcmp(mode, "tlb")) {
     // 2 MiB-page aliasing test: pads that move each chunk to another 2 MiB page index
