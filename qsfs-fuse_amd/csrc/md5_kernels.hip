@@ -13,6 +13,9 @@
 //                            coalesced LDS-DMA staging of 128 B per chain.
 //   qsmd5_batch_kernel       throughput kernel, more chunks, any alignment:
 //                            per-lane loads, 5 VALU per step.
+//   qsmd5_column_pc[2]_kernel  the latency kernels over one column of a
+//                            host-staged batch: chains resume from and park in
+//                            HBM state (qsmd5_runtime.cpp run_batch).
 // Streaming kernels (the MD5 class, MD5.cpp:240-312):
 //   qsmd5_blocks_kernel      advances one state over whole blocks (update()).
 //   qsmd5_final_kernel       tail + padding + length (finalize()).

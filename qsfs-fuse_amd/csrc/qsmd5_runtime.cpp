@@ -156,6 +156,7 @@ struct Dev {
 struct Runtime {
   bool ready = false;
   int init_rc = 0;
+  std::string init_msg;         // why init failed, for callers on other threads
   std::vector<Dev*> devs;       // devs[0] = primary (ctx, device-async, fill)
   uint64_t shard_bytes = 0;     // host bytes per extra GPU before a batch is sharded
   std::mutex timing_mu;
@@ -226,17 +227,20 @@ void do_init() {
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n <= 0) {
     r.init_rc = fail(-ENODEV, "qsmd5: no usable GPU (hipGetDeviceCount)");
+    r.init_msg = t_last_error;
     return;
   }
   std::vector<int> ords;
   if (int rc = parse_devices(n, &ords)) {
     r.init_rc = rc;
+    r.init_msg = t_last_error;
     return;
   }
   for (int o : ords) {
     Dev* d = new Dev;
     if (int rc = init_dev(*d, o)) {
       r.init_rc = rc;
+      r.init_msg = t_last_error;
       return;  // partially built Devs are leaked with the runtime: init failed for good
     }
     r.devs.push_back(d);
@@ -250,7 +254,7 @@ void do_init() {
 int ensure_init() {
   std::call_once(g_init_once, do_init);
   Runtime& r = rt();
-  if (!r.ready) return r.init_rc ? r.init_rc : -ENODEV;
+  if (!r.ready) return fail(r.init_rc ? r.init_rc : -ENODEV, r.init_msg);
   // Calls may come from threads whose current device differs.
   int cur = -1;
   if (hipGetDevice(&cur) != hipSuccess || cur != r.devs[0]->device) {
