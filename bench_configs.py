@@ -301,6 +301,8 @@ def main():
             config3(args.reps)
         elif c == "small":
             many_small(args.reps)
+        elif c == "5h":
+            config3(args.reps, n=10000, label=" -- BASELINE config 5 host-resident (97.7 GiB)")
         elif c == "3p":
             config3_pageable(args.reps)
         elif c == "4":
