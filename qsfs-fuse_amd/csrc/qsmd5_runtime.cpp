@@ -753,6 +753,8 @@ struct Coalescer {
   std::condition_variable cv;
   Request* head = nullptr;
   Request* tail = nullptr;
+  size_t queued = 0;      // requests in the list
+  size_t prev_group = 0;  // requests the previous leader ran
   bool busy = false;
 };
 
@@ -842,27 +844,41 @@ int group_commit(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], in
   if (env_u64("QSMD5_NO_COALESCE", 0)) return run_any(chunks, n, digests, flags);
   Coalescer& co = coalescer();
   Request req{chunks, n, digests, flags};
+  // Linger: callers released by the previous launch usually re-submit within
+  // microseconds (a worker loop hashing part after part).  A new leader waits
+  // up to this long for as many requests as the previous group held, so they
+  // ride in this launch instead of the next one; a lone caller never waits.
+  static const std::chrono::microseconds linger(env_u64("QSMD5_COALESCE_LINGER_US", 300));
   std::unique_lock<std::mutex> lk(co.mu);
   if (co.tail) co.tail->next = &req;
   else co.head = &req;
   co.tail = &req;
+  ++co.queued;
+  co.cv.notify_all();  // a lingering leader counts arrivals
   while (!req.done) {
     if (co.busy) {
       co.cv.wait(lk);
       continue;
     }
-    // Lead: take the queue's head requests (FIFO) up to kMaxGroupChunks, at least one.
     co.busy = true;
+    if (co.prev_group > 1 && co.queued < co.prev_group && linger.count() > 0) {
+      const size_t want = co.prev_group;
+      co.cv.wait_for(lk, linger, [&] { return co.queued >= want; });
+    }
+    // Lead: take the queue's head requests (FIFO) up to kMaxGroupChunks, at least one.
     Request* first = co.head;
     Request* last = first;
-    size_t total = first->n;
+    size_t total = first->n, taken = 1;
     while (last->next && total + last->next->n <= kMaxGroupChunks) {
       last = last->next;
       total += last->n;
+      ++taken;
     }
     co.head = last->next;
     if (!co.head) co.tail = nullptr;
     last->next = nullptr;
+    co.queued -= taken;
+    co.prev_group = taken;
     lk.unlock();
     run_group(first);
     lk.lock();

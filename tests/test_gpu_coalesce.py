@@ -9,7 +9,10 @@ is busy into the next launch.  Checked here:
   re-run request by request);
 - the REF_TRUNCATE32 flag stays per caller inside a merged batch;
 - concurrent one-part calls finish in far less time than the same calls
-  serialised (QSMD5_NO_COALESCE=1), measured in child processes.
+  serialised (QSMD5_NO_COALESCE=1), measured in child processes;
+- native callers in a tight loop (tests/cpp/coalesce_bench, qsfs's executor
+  threads calling md5() part after part): the leader's linger lets the callers
+  released by one launch ride in the next.
 """
 import ctypes
 import json
@@ -109,11 +112,13 @@ print(json.dumps({"wall_s": time.perf_counter() - t0, "ok": got == want}))
 '''
 
 
-def _timed(no_coalesce):
+def _timed(no_coalesce, linger_us=None):
     env = dict(os.environ, PYTHONPATH=os.pathsep.join(
         [os.path.join(ROOT, "qsfs-fuse_amd"), os.path.join(ROOT, "tests")]))
     if no_coalesce:
         env["QSMD5_NO_COALESCE"] = "1"
+    if linger_us is not None:
+        env["QSMD5_COALESCE_LINGER_US"] = str(linger_us)
     out = subprocess.run([sys.executable, "-c", TIMING_SCRIPT], env=env, capture_output=True,
                          text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr[-3000:]
@@ -122,9 +127,38 @@ def _timed(no_coalesce):
 
 def test_coalescing_beats_serialised_calls():
     ser = _timed(True)
+    co0 = _timed(False, linger_us=0)
     co = _timed(False)
-    assert ser["ok"] and co["ok"]
+    assert ser["ok"] and co0["ok"] and co["ok"]
     # 12 one-part calls from 6 threads: serialised = 12 chain times (~1 s);
-    # merged = a few launches
-    print("serialised %.3f s, coalesced %.3f s" % (ser["wall_s"], co["wall_s"]))
+    # merged = a few launches; with the linger, a worker released by one launch
+    # rides in the next instead of the one after
+    print("serialised %.3f s, coalesced without linger %.3f s, with linger %.3f s"
+          % (ser["wall_s"], co0["wall_s"], co["wall_s"]))
+    assert co0["wall_s"] < 0.6 * ser["wall_s"], (ser, co0)
     assert co["wall_s"] < 0.6 * ser["wall_s"], (ser, co)
+
+
+def _native(env_extra):
+    exe = os.path.join(ROOT, "tests", "cpp", "coalesce_bench")
+    if not os.path.exists(exe):
+        subprocess.check_call([
+            "g++", "-std=c++17", "-O2", os.path.join(ROOT, "tests", "cpp", "coalesce_bench.cpp"),
+            "-I" + os.path.join(ROOT, "include"), "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"),
+            "-lqsmd5", "-lpthread", "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"),
+            "-o", exe])
+    env = dict(os.environ, **env_extra)
+    out = subprocess.run([exe, "5", "6"], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr[-2000:]
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_native_callers_linger():
+    no_linger = _native({"QSMD5_COALESCE_LINGER_US": "0"})
+    linger = _native({})
+    ser = _native({"QSMD5_NO_COALESCE": "1"})
+    print("5 native threads x 6 parts: serialised %.3f s, no linger %.3f s, linger %.3f s"
+          % (ser["wall_s"], no_linger["wall_s"], linger["wall_s"]))
+    assert ser["ok"] and no_linger["ok"] and linger["ok"]
+    assert linger["wall_s"] < 0.85 * no_linger["wall_s"], (no_linger, linger)
+    assert no_linger["wall_s"] < 0.6 * ser["wall_s"], (ser, no_linger)
