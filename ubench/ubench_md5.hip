@@ -239,6 +239,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 6)
       hipLaunchKernelGGL(k_coal_imm, dim3(grid), dim3(64), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig);
+
     else
       hipLaunchKernelGGL(k_pc_depth<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
@@ -261,11 +262,12 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   med = s[s.size() / 2];
   double gib = (double)L * B / (1u << 30);
   if (pad) printf("(stride pad %llu) ", (unsigned long long)pad);
-  if ((which == 1 || which == 3 || which == 4 || which == 5) && g_skew) printf("(skew %u) ", g_skew);
+  if ((which == 1 || which == 3 || which == 4 || which == 5 || which == 7) && g_skew)
+    printf("(skew %u) ", g_skew);
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 7 ? "pc-p2" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -342,6 +344,7 @@ static int run_edges(int which) {
   else if (which == 6)
     hipLaunchKernelGGL(k_coal_imm, dim3((n + 63) / 64), dim3(64), 0, 0, dd, nullptr, (uint32_t)n,
                        dg);
+
   else
     hipLaunchKernelGGL(k_pc_depth<3>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew);
@@ -750,6 +753,19 @@ int main(int argc, char** argv) {
     }
     run_md5(512, 32ull << 20, 2, false, 0, 0);
     run_md5(512, 32ull << 20, 2, false, 0, 4096);
+    return 0;
+  }
+  if (!strcmp(mode, "footprint")) {
+    // 10 MiB chunks dense vs spread at a 32/64 MiB + 4 KiB stride; 10 000 dense
+    // chunks (98 GiB footprint).  A two-producer-wave variant of the latency
+    // kernel was measured here and dropped (profiles/r01_ubench_footprint_producers.log).
+    for (int rep = 0; rep < 2; ++rep) {
+      run_md5(512, 10ull << 20, 2, rep == 0, 1, 0);
+      run_md5(512, 10ull << 20, 2, rep == 0, 1, (54ull << 20) + 4096);
+      run_md5(512, 10ull << 20, 2, false, 1, (22ull << 20) + 4096);
+      run_md5(512, 64ull << 20, 2, false, 1, 4096);
+    }
+    run_md5(10000, 10ull << 20, 2, true, 1, 0);
     return 0;
   }
   if (!strcmp(mode, "imm")) {
