@@ -1,0 +1,135 @@
+// qsfs-fuse_amd/csrc/qsmd5_plan.h -- the staging plan for host-resident chunks.
+//
+// Pure host logic (no HIP), shared by the runtime (qsmd5_runtime.cpp run_batch)
+// and the CPU tests (tests/cpp/test_plan.cpp), which check its invariants.
+//
+// Host-resident chunks (the qsfs case: parts in pooled host buffers,
+// ResourceManager.cpp:53-77) are staged into a device ring in SLICES.  The
+// chunks, sorted by length (descending), form GROUPS that fit one ring region;
+// a group is cut into COLUMNS of width W: column j of a group is bytes
+// [jW, (j+1)W) of each of its chunks still that long.  One slice = one
+// (group, column): one H2D transfer into a region, then one kernel launch that
+// resumes each chain from its parked state.  Columns let every chain start as
+// soon as the first column lands, so the serial chain of the LAST chunk copied
+// no longer trails the transfer: only its last column (~8 ms at W ~ 1 MiB)
+// does.  W = kNoColumns (chunks no longer than a column) degenerates to
+// whole-chunk row slices.
+//
+// Staged segments are packed at 256-B alignment plus a 4 KiB + 256 B skew, so
+// that equal-size parts never sit at a power-of-two stride (the lanes of a
+// wave walk their chunks in lockstep; a power-of-two stride sends every lane's
+// request to the same HBM channel).
+#pragma once
+
+#include <stdint.h>
+
+#include <algorithm>
+#include <vector>
+
+namespace qsmd5 {
+
+constexpr uint64_t kSliceMin = 512ull << 20;  // automatic slice target bounds
+constexpr uint64_t kSliceMax = 4ull << 30;
+constexpr uint64_t kAlign = 256;
+constexpr uint64_t kSkew = 4096 + 256;
+constexpr uint64_t kColGrain = 64ull << 10;  // automatic column widths are multiples of this
+constexpr uint64_t kColMin = 1ull << 20;     // ... and at least this (>= 1 MiB per-chunk copies)
+constexpr uint64_t kNoColumns = ~0ull;
+
+// Bytes one staged segment of L message bytes occupies in a region.
+inline uint64_t stage_bytes(uint64_t L) { return ((L + kAlign - 1) & ~(kAlign - 1)) + kSkew; }
+
+struct Group {
+  size_t first, count;  // range in the host lane order
+  uint32_t ncols;
+};
+
+struct Slice {
+  size_t group;
+  uint32_t col;
+  size_t active;  // chunks of the group still live in this column (a prefix)
+  size_t seg0;    // first entry in the segment/order arrays (multi-column groups)
+};
+
+struct HostPlan {
+  uint64_t W = kNoColumns;  // column width, or kNoColumns
+  uint64_t slice_target = 0;
+  uint64_t region = 0;      // bytes of one ring region
+  size_t nregions = 0;      // regions in the ring (slice s uses region s % nregions)
+  size_t nseg = 0;          // segment descriptors of multi-column groups
+  std::vector<Group> groups;
+  std::vector<Slice> slices;
+
+  // Message bytes of a chunk of length L in column j.
+  uint64_t col_bytes(uint64_t L, uint32_t j) const {
+    if (W == kNoColumns) return j == 0 ? L : 0;
+    const uint64_t o = (uint64_t)j * W;
+    return L > o ? std::min(W, L - o) : 0;
+  }
+};
+
+// host_len: lengths (>= 1) of the host chunks in lane order, longest first.
+// staging_cap: bytes of device memory the ring may use.
+// slice_bytes: slice target, 0 = automatic (a quarter of the batch, clamped to
+//   [kSliceMin, kSliceMax]).
+// column_bytes: < 0 automatic (one column of every chunk fills about one
+//   slice; a multiple of kColGrain, at least kColMin); 0 = whole chunks;
+//   > 0 forced (rounded down to a multiple of 64, at least 64).
+inline HostPlan plan_host(const std::vector<uint64_t>& host_len, uint64_t staging_cap,
+                          uint64_t slice_bytes, int64_t column_bytes) {
+  HostPlan P;
+  if (host_len.empty()) return P;
+  uint64_t host_total = 0;
+  const uint64_t max_host = host_len.front();
+  for (uint64_t L : host_len) host_total += stage_bytes(L);
+  P.slice_target =
+      slice_bytes ? slice_bytes : std::min(kSliceMax, std::max(kSliceMin, host_total / 4));
+  uint64_t w;
+  if (column_bytes < 0) {
+    const uint64_t per = P.slice_target / host_len.size();
+    w = per > kSkew + kAlign ? (per - kSkew - kAlign) / kColGrain * kColGrain : 0;
+    w = std::max(w, kColMin);
+  } else if (column_bytes == 0) {
+    w = kNoColumns;
+  } else {
+    w = std::max<uint64_t>(64, (uint64_t)column_bytes & ~63ull);
+  }
+  if (w < max_host) P.W = w;
+  // A region holds one column of a whole group.  When the column width sits
+  // at its floor (kColMin) the chunks' first columns may overshoot the slice
+  // target slightly; grow the region (up to half the ring) rather than split
+  // off a small second group whose columns would all trail the first.
+  uint64_t first_cols = 0;
+  for (uint64_t L : host_len) first_cols += stage_bytes(P.col_bytes(L, 0));
+  P.region = std::max<uint64_t>({P.slice_target, stage_bytes(P.col_bytes(max_host, 0)),
+                                 P.W == kNoColumns ? 0 : std::min<uint64_t>(first_cols, staging_cap / 2)});
+  for (size_t k = 0; k < host_len.size();) {
+    Group g{k, 0, 1};
+    uint64_t bytes = 0;
+    while (k < host_len.size()) {
+      const uint64_t b = stage_bytes(P.col_bytes(host_len[k], 0));
+      if (g.count > 0 && bytes + b > P.region) break;
+      bytes += b;
+      ++g.count;
+      ++k;
+    }
+    const uint64_t longest = host_len[g.first];
+    if (P.W != kNoColumns) g.ncols = (uint32_t)std::max<uint64_t>(1, (longest + P.W - 1) / P.W);
+    P.groups.push_back(g);
+  }
+  for (size_t gi = 0; gi < P.groups.size(); ++gi) {
+    const Group& g = P.groups[gi];
+    for (uint32_t j = 0; j < g.ncols; ++j) {
+      size_t act = 0;
+      while (act < g.count && P.col_bytes(host_len[g.first + act], j) > 0) ++act;
+      P.slices.push_back(Slice{gi, j, act, P.nseg});
+      if (g.ncols > 1) P.nseg += act;
+    }
+  }
+  const uint64_t cap = std::min<uint64_t>(staging_cap, host_total + P.region);
+  P.nregions = (size_t)std::max<uint64_t>(1, cap / P.region);
+  P.nregions = std::min(P.nregions, P.slices.size());
+  return P;
+}
+
+}  // namespace qsmd5

@@ -35,6 +35,7 @@
 
 #include "../../include/qsmd5.h"
 #include "md5_launch.h"
+#include "qsmd5_plan.h"
 
 namespace {
 
@@ -46,13 +47,8 @@ using qsmd5::kKernelThroughput;
 constexpr uint64_t kMaxChunkLen = 1ull << 38;
 constexpr int kComputeStreams = 8;
 constexpr int kMaxCopyStreams = 4;
-constexpr uint64_t kSliceMin = 512ull << 20;        // H2D slice bounds
-constexpr uint64_t kSliceMax = 4ull << 30;
 constexpr uint64_t kDefaultStaging = 16ull << 30;   // device staging ring
-constexpr uint64_t kAlign = 256;
-constexpr uint64_t kSkew = 4096 + 256;
 
-inline uint64_t stage_bytes(uint64_t L) { return ((L + kAlign - 1) & ~(kAlign - 1)) + kSkew; }
 
 thread_local std::string t_last_error;
 
@@ -300,29 +296,8 @@ int kernel_choice(size_t n, bool aligned16) {
   return aligned16 ? kKernelCoalesced : kKernelThroughput;
 }
 
-// Host-resident chunks are staged in SLICES.  Chunks (sorted by length) form
-// GROUPS that fit one staging region; a group is cut into COLUMNS of width W:
-// column j of a group is bytes [jW, (j+1)W) of each of its chunks still that
-// long.  One slice = one (group, column): one H2D transfer into a ring region,
-// then one kernel launch that resumes each chain from its parked state.
-// Columns let every chain start as soon as the first column lands, so the
-// serial chain of the LAST chunk copied no longer trails the transfer: only
-// its last column (~8 ms at W ~ 1 MiB) does.  W = ~0 (chunks no longer than
-// the column) degenerates to whole-chunk row slices.
-struct Group {
-  size_t first, count;  // range in host_idx
-  uint32_t ncols;
-};
-struct Slice {
-  size_t group;
-  uint32_t col;
-  size_t active;  // chunks of the group still live in this column (a prefix)
-  size_t seg0;    // first entry in the segment/order arrays (multi-column groups)
-};
-
-constexpr uint64_t kColGrain = 64ull << 10;  // automatic column widths are multiples of this
-constexpr uint64_t kColMin = 1ull << 20;     // ... and at least this (>= 1 MiB per-chunk copies)
-constexpr uint64_t kNoColumns = ~0ull;
+using qsmd5::kNoColumns;
+using qsmd5::stage_bytes;
 
 // The synchronous batch on one GPU: device chunks in one launch; host chunks
 // staged in slices with copy/compute overlap.  Caller holds r.mu and has made
@@ -334,7 +309,6 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
 
   std::vector<uint64_t> len(n);
   std::vector<MemKind> kind(n);
-  uint64_t max_host = 0, host_total = 0;
   for (size_t i = 0; i < n; ++i) {
     uint64_t L = chunks[i].len;
     if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;
@@ -346,10 +320,6 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     if (L && kind[i] == kDeviceMem && owner != r.device)
       return fail(-EINVAL, "qsmd5: chunk lives on GPU " + std::to_string(owner) +
                                ", not on a bound GPU (QSMD5_DEVICE/QSMD5_DEVICES)");
-    if (kind[i] == kHostMem) {
-      max_host = std::max(max_host, L);
-      host_total += stage_bytes(L);
-    }
   }
 
   const auto t_classified = std::chrono::steady_clock::now();
@@ -362,67 +332,22 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   std::sort(host_idx.begin(), host_idx.end(), by_len);
 
   const auto t_sorted = std::chrono::steady_clock::now();
-  // Column width: one column of every host chunk should fill about one slice.
-  const uint64_t slice_target = env_u64(
-      "QSMD5_SLICE_BYTES", std::min(kSliceMax, std::max(kSliceMin, host_total / 4)));
-  uint64_t W = kNoColumns;
-  if (!host_idx.empty()) {
-    const uint64_t per = slice_target / host_idx.size();
-    uint64_t w = per > kSkew + kAlign ? (per - kSkew - kAlign) / kColGrain * kColGrain : 0;
-    w = std::max(w, kColMin);
-    if (const char* ev = getenv("QSMD5_COLUMN_BYTES"); ev && *ev) {
-      const uint64_t forced = env_u64("QSMD5_COLUMN_BYTES", 0);  // 0 = whole chunks
-      w = forced ? std::max<uint64_t>(64, forced & ~63ull) : kNoColumns;
-    }
-    if (w < max_host) W = w;
-  }
-  auto col_bytes = [&](uint64_t L, uint32_t j) -> uint64_t {  // chunk bytes in column j
-    if (W == kNoColumns) return j == 0 ? L : 0;
-    const uint64_t o = (uint64_t)j * W;
-    return L > o ? std::min(W, L - o) : 0;
-  };
-  // A region holds one column of a whole group.  When the column width sits at
-  // its floor (kColMin) the host chunks' first columns may overshoot the slice
-  // target slightly; grow the region (up to half the staging ring) rather than
-  // splitting off a small second group whose columns would all trail the first.
-  uint64_t first_cols = 0;
-  for (uint32_t ci : host_idx) first_cols += stage_bytes(col_bytes(len[ci], 0));
-  const uint64_t region = std::max<uint64_t>(
-      {slice_target, stage_bytes(col_bytes(max_host, 0)),
-       W == kNoColumns ? 0 : std::min<uint64_t>(first_cols, r.staging_cap / 2)});
-  std::vector<Group> groups;
-  for (size_t k = 0; k < host_idx.size();) {
-    Group g{k, 0, 1};
-    uint64_t bytes = 0;
-    while (k < host_idx.size()) {
-      const uint64_t b = stage_bytes(col_bytes(len[host_idx[k]], 0));
-      if (g.count > 0 && bytes + b > region) break;
-      bytes += b;
-      ++g.count;
-      ++k;
-    }
-    const uint64_t longest = len[host_idx[g.first]];
-    if (W != kNoColumns) g.ncols = (uint32_t)std::max<uint64_t>(1, (longest + W - 1) / W);
-    groups.push_back(g);
-  }
-  std::vector<Slice> slices;
-  size_t nseg = 0;
-  for (size_t gi = 0; gi < groups.size(); ++gi) {
-    const Group& g = groups[gi];
-    for (uint32_t j = 0; j < g.ncols; ++j) {
-      size_t act = 0;
-      while (act < g.count && col_bytes(len[host_idx[g.first + act]], j) > 0) ++act;
-      slices.push_back(Slice{gi, j, act, nseg});
-      if (g.ncols > 1) nseg += act;
-    }
-  }
-  size_t nregions = 0;
-  if (!slices.empty()) {
-    uint64_t cap = std::min<uint64_t>(r.staging_cap, host_total + region);
-    nregions = (size_t)std::max<uint64_t>(1, cap / region);
-    nregions = std::min(nregions, slices.size());
+  // Staging plan for the host chunks (qsmd5_plan.h; its invariants are tested
+  // on the CPU by tests/cpp/test_plan.cpp).
+  std::vector<uint64_t> host_len(host_idx.size());
+  for (size_t k = 0; k < host_idx.size(); ++k) host_len[k] = len[host_idx[k]];
+  int64_t column_bytes = -1;  // automatic
+  if (const char* ev = getenv("QSMD5_COLUMN_BYTES"); ev && *ev)
+    column_bytes = (int64_t)env_u64("QSMD5_COLUMN_BYTES", 0);  // 0 = whole chunks
+  const qsmd5::HostPlan plan =
+      qsmd5::plan_host(host_len, r.staging_cap, env_u64("QSMD5_SLICE_BYTES", 0), column_bytes);
+  const uint64_t W = plan.W, region = plan.region;
+  const std::vector<qsmd5::Group>& groups = plan.groups;
+  const std::vector<qsmd5::Slice>& slices = plan.slices;
+  const size_t nseg = plan.nseg, nregions = plan.nregions;
+  auto col_bytes = [&](uint64_t L, uint32_t j) { return plan.col_bytes(L, j); };
+  if (!slices.empty())
     if (int rc = r.d_staging.reserve(nregions * region)) return rc;
-  }
 
   // Descriptors (device pointers) for every chunk, upfront; segment
   // descriptors and lane->chunk maps for the multi-column slices behind them.
@@ -444,8 +369,8 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   uint8_t* stage = static_cast<uint8_t*>(r.d_staging.p);
   std::vector<uint8_t*> slice_base(slices.size());
   for (size_t si = 0; si < slices.size(); ++si) {
-    const Slice& sl = slices[si];
-    const Group& g = groups[sl.group];
+    const qsmd5::Slice& sl = slices[si];
+    const qsmd5::Group& g = groups[sl.group];
     uint8_t* base = stage + (si % nregions) * region;
     slice_base[si] = base;
     uint64_t off = 0;
@@ -520,8 +445,8 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   // descriptors have landed.  Runs of equal-length chunks at a constant host
   // stride (a file's parts) go as one 2-D copy per column.
   for (size_t si = 0; si < slices.size(); ++si) {
-    const Slice& sl = slices[si];
-    const Group& g = groups[sl.group];
+    const qsmd5::Slice& sl = slices[si];
+    const qsmd5::Group& g = groups[sl.group];
     const size_t reg = si % nregions;
     hipStream_t cs = r.compute[1 + sl.group % (kComputeStreams - 1)];
     hipStream_t cp = r.copy[si % r.ncopy];

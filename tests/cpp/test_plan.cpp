@@ -1,0 +1,173 @@
+// tests/cpp/test_plan.cpp -- CPU checks of the host-staging plan
+// (qsfs-fuse_amd/csrc/qsmd5_plan.h, used by qsmd5_runtime.cpp run_batch).
+//
+// For many length mixes (qsfs part sets, ragged, tiny, one huge chunk), ring
+// sizes, slice targets and column widths, the plan must:
+//   1. cut the host chunks (lane order, longest first) into contiguous groups;
+//   2. stage every byte of every chunk exactly once: the columns of a chunk
+//      are [jW, (j+1)W) clipped to its length, for j = 0 .. ncols - 1;
+//   3. make each slice's active chunks the prefix of its group still live in
+//      that column, with active > 0 (no empty launches);
+//   4. fit every slice in one region, and the ring in the staging cap unless a
+//      single slice alone is larger (then one region of that size);
+//   5. use columns only when some chunk is longer than W; W a multiple of 64,
+//      and of 64 KiB (>= 1 MiB) when automatic;
+//   6. number the segment descriptors of multi-column groups densely (nseg).
+// Prints "plan ok <cases>" and exits 0, or the first violation and exits 1.
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <cmath>
+#include <random>
+#include <vector>
+
+#include "../../qsfs-fuse_amd/csrc/qsmd5_plan.h"
+
+using namespace qsmd5;
+
+static int fails = 0;
+#define CHECK(cond, ...)                        \
+  do {                                          \
+    if (!(cond)) {                              \
+      if (fails++ < 10) {                       \
+        fprintf(stderr, "FAIL %s: ", #cond);    \
+        fprintf(stderr, __VA_ARGS__);           \
+        fprintf(stderr, "\n");                  \
+      }                                         \
+    }                                           \
+  } while (0)
+
+static void check(const std::vector<uint64_t>& len, uint64_t cap, uint64_t slice, int64_t col,
+                  const char* what) {
+  const HostPlan P = plan_host(len, cap, slice, col);
+  if (len.empty()) {
+    CHECK(P.slices.empty() && P.groups.empty(), "%s: empty input", what);
+    return;
+  }
+  const uint64_t longest = len.front();
+  // 5. column width
+  if (P.W != kNoColumns) {
+    CHECK(P.W < longest, "%s: W %llu not below the longest chunk", what, (unsigned long long)P.W);
+    CHECK(P.W % 64 == 0, "%s: W %llu not a multiple of 64", what, (unsigned long long)P.W);
+    if (col < 0)
+      CHECK(P.W % kColGrain == 0 && P.W >= kColMin, "%s: automatic W %llu", what,
+            (unsigned long long)P.W);
+  } else {
+    CHECK(col == 0 || (col < 0) || (uint64_t)std::max<int64_t>(64, col & ~63ll) >= longest,
+          "%s: no columns although forced width %lld < longest", what, (long long)col);
+    for (const Group& g : P.groups) CHECK(g.ncols == 1, "%s: ncols %u without columns", what, g.ncols);
+  }
+  // 1. groups partition [0, n) contiguously
+  size_t next = 0;
+  for (const Group& g : P.groups) {
+    CHECK(g.first == next && g.count > 0, "%s: group at %zu count %zu, expected start %zu", what,
+          g.first, g.count, next);
+    next = g.first + g.count;
+    const uint64_t want_cols =
+        P.W == kNoColumns ? 1 : std::max<uint64_t>(1, (len[g.first] + P.W - 1) / P.W);
+    CHECK(g.ncols == want_cols, "%s: group ncols %u, want %llu", what, g.ncols,
+          (unsigned long long)want_cols);
+  }
+  CHECK(next == len.size(), "%s: groups cover %zu of %zu chunks", what, next, len.size());
+  // 2, 3, 4, 6 per slice
+  std::vector<uint64_t> staged(len.size(), 0);
+  std::vector<uint32_t> next_col(P.groups.size(), 0);
+  size_t seg = 0;
+  uint64_t max_slice_bytes = 0;
+  for (const Slice& sl : P.slices) {
+    CHECK(sl.group < P.groups.size(), "%s: slice group %zu", what, sl.group);
+    const Group& g = P.groups[sl.group];
+    CHECK(sl.col == next_col[sl.group], "%s: group %zu column %u out of order", what, sl.group, sl.col);
+    next_col[sl.group] = sl.col + 1;
+    CHECK(sl.active > 0 && sl.active <= g.count, "%s: active %zu of %zu", what, sl.active, g.count);
+    uint64_t bytes = 0;
+    for (size_t k = 0; k < g.count; ++k) {
+      const uint64_t b = P.col_bytes(len[g.first + k], sl.col);
+      if (k < sl.active) {
+        CHECK(b > 0, "%s: active chunk %zu has no bytes in column %u", what, g.first + k, sl.col);
+        CHECK(b == std::min(P.W == kNoColumns ? len[g.first + k] : P.W,
+                            len[g.first + k] - (P.W == kNoColumns ? 0 : (uint64_t)sl.col * P.W)),
+              "%s: column bytes", what);
+        staged[g.first + k] += b;
+        bytes += stage_bytes(b);
+      } else {
+        CHECK(b == 0, "%s: chunk %zu live in column %u but outside the active prefix", what,
+              g.first + k, sl.col);
+      }
+    }
+    CHECK(bytes <= P.region, "%s: slice needs %llu B > region %llu B", what,
+          (unsigned long long)bytes, (unsigned long long)P.region);
+    max_slice_bytes = std::max(max_slice_bytes, bytes);
+    if (g.ncols > 1) {
+      CHECK(sl.seg0 == seg, "%s: seg0 %zu, want %zu", what, sl.seg0, seg);
+      seg += sl.active;
+    }
+  }
+  for (size_t gi = 0; gi < P.groups.size(); ++gi)
+    CHECK(next_col[gi] == P.groups[gi].ncols, "%s: group %zu has %u of %u columns", what, gi,
+          next_col[gi], P.groups[gi].ncols);
+  CHECK(seg == P.nseg, "%s: nseg %zu, want %zu", what, P.nseg, seg);
+  for (size_t i = 0; i < len.size(); ++i)
+    CHECK(staged[i] == len[i], "%s: chunk %zu staged %llu of %llu B", what, i,
+          (unsigned long long)staged[i], (unsigned long long)len[i]);
+  CHECK(P.nregions >= 1 && P.nregions <= P.slices.size(), "%s: nregions %zu", what, P.nregions);
+  CHECK(P.nregions * P.region <= std::max(cap, P.region), "%s: ring %llu B over cap %llu B", what,
+        (unsigned long long)(P.nregions * P.region), (unsigned long long)cap);
+}
+
+int main() {
+  const uint64_t MiB = 1ull << 20, GiB = 1ull << 30;
+  std::mt19937_64 rng(1234);
+  int cases = 0;
+  auto run = [&](std::vector<uint64_t> len, const char* what) {
+    std::sort(len.begin(), len.end(), [](uint64_t a, uint64_t b) { return a > b; });
+    for (uint64_t cap : {256 * MiB, 2 * GiB, 16 * GiB})
+      for (uint64_t slice : {(uint64_t)0, 64 * MiB, 1 * GiB})
+        for (int64_t col : {(int64_t)-1, (int64_t)0, (int64_t)64, (int64_t)192, (int64_t)4160,
+                            (int64_t)1 << 20, (int64_t)3000}) {
+          // forced tiny columns on long chunks: millions of slices; keep the
+          // checker's work (columns x chunks) bounded
+          if (col > 0 && !len.empty() &&
+              (double)(len.front() / (uint64_t)std::max<int64_t>(64, col) + 1) * len.size() > 3e6)
+            continue;
+          check(len, cap, slice, col, what);
+          ++cases;
+        }
+  };
+  run({}, "empty");
+  run({1}, "one byte");
+  run({10 * MiB}, "one part");
+  run(std::vector<uint64_t>(512, 10 * MiB), "512 x 10 MiB");
+  run(std::vector<uint64_t>(4096, 10 * MiB), "4096 x 10 MiB");
+  {
+    std::vector<uint64_t> v(10, 10 * MiB);  // PrepareUpload of 100 MiB + 12345 B: averaged pair
+    v.push_back(5 * MiB + 6172);
+    v.push_back(5 * MiB + 6173);
+    run(v, "file parts with averaged tail");
+  }
+  {
+    std::vector<uint64_t> v;
+    for (int i = 0; i < 700; ++i) {  // log-uniform 8 KiB .. 64 MiB, as the ragged fixture
+      const double e = 13.0 + (26.0 - 13.0) * (double)(rng() % 100000) / 100000.0;
+      v.push_back((uint64_t)std::max(1.0, std::exp2(e)) + rng() % 97);
+    }
+    run(v, "ragged 8 KiB..64 MiB");
+  }
+  {
+    std::vector<uint64_t> v;
+    for (int i = 0; i < 3000; ++i) v.push_back(1 + rng() % 5000);
+    run(v, "3000 tiny");
+  }
+  {
+    std::vector<uint64_t> v(200, 64 * MiB);
+    v.push_back(3 * GiB);  // one chunk much longer than the rest
+    run(v, "one huge chunk");
+  }
+  for (int t = 0; t < 40; ++t) {
+    std::vector<uint64_t> v(1 + rng() % 300);
+    for (auto& L : v) L = 1 + rng() % (1 + (rng() % 4 == 0 ? 200 * MiB : 3 * MiB));
+    run(v, "random mix");
+  }
+  printf("plan %s %d cases\n", fails ? "FAIL" : "ok", cases);
+  return fails ? 1 : 0;
+}
