@@ -132,4 +132,30 @@ inline HostPlan plan_host(const std::vector<uint64_t>& host_len, uint64_t stagin
   return P;
 }
 
+// Multi-GPU split of host chunks (qsmd5_runtime.cpp run_sharded): the chunks
+// (in caller order, lengths host_len) go in contiguous, byte-balanced ranges to
+// k = min(ndev, ceil(total / shard_bytes)) GPUs; a small batch stays on one
+// GPU (a chain costs the same on any number of GPUs; only the host link time
+// shrinks with more).  Returns the shard index of each chunk (0 .. k-1), and
+// k in *nshards.
+inline std::vector<uint32_t> plan_shards(const std::vector<uint64_t>& host_len, size_t ndev,
+                                         uint64_t shard_bytes, size_t* nshards) {
+  uint64_t total = 0;
+  for (uint64_t L : host_len) total += L;
+  const uint64_t per = std::max<uint64_t>(1, shard_bytes);
+  const size_t k = (size_t)std::min<uint64_t>(std::max<size_t>(1, ndev),
+                                              std::max<uint64_t>(1, (total + per - 1) / per));
+  std::vector<uint32_t> shard(host_len.size(), 0);
+  uint64_t cum = 0;
+  size_t sh = 0;
+  for (size_t i = 0; i < host_len.size(); ++i) {
+    // shard sh takes chunks while the bytes before them are below its share
+    while (sh + 1 < k && cum >= total / k * (sh + 1)) ++sh;
+    shard[i] = (uint32_t)sh;
+    cum += host_len[i];
+  }
+  if (nshards) *nshards = k;
+  return shard;
+}
+
 }  // namespace qsmd5

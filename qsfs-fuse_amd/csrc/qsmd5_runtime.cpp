@@ -565,7 +565,6 @@ int run_sharded(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
   const size_t nd = R.devs.size();
   std::vector<std::vector<uint32_t>> part(nd);
   std::vector<uint32_t> host;
-  uint64_t host_bytes = 0;
   if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
   for (size_t i = 0; i < n; ++i) {
     uint64_t L = chunks[i].len;
@@ -580,21 +579,17 @@ int run_sharded(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
       part[d].push_back((uint32_t)i);
     } else {
       host.push_back((uint32_t)i);
-      host_bytes += L;
     }
   }
-  const uint64_t per = std::max<uint64_t>(1, R.shard_bytes);
-  const size_t k = (size_t)std::min<uint64_t>(nd, std::max<uint64_t>(1, (host_bytes + per - 1) / per));
-  uint64_t cum = 0;
-  size_t sh = 0;
-  for (uint32_t i : host) {
-    uint64_t L = chunks[i].len;
+  std::vector<uint64_t> host_len(host.size());
+  for (size_t j = 0; j < host.size(); ++j) {
+    uint64_t L = chunks[host[j]].len;
     if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;
-    // shard sh takes chunks while the bytes before them are below its share
-    while (sh + 1 < k && cum >= host_bytes / k * (sh + 1)) ++sh;
-    part[sh].push_back(i);
-    cum += L;
+    host_len[j] = L;
   }
+  size_t k = 1;
+  const std::vector<uint32_t> shard = qsmd5::plan_shards(host_len, nd, R.shard_bytes, &k);
+  for (size_t j = 0; j < host.size(); ++j) part[shard[j]].push_back(host[j]);
   if (env_u64("QSMD5_TRACE", 0)) {
     for (size_t d = 0; d < nd; ++d)
       fprintf(stderr, "qsmd5 shard: context %zu (GPU %d) takes %zu chunks\n", d, R.devs[d]->device,

@@ -12,7 +12,10 @@
 //      single slice alone is larger (then one region of that size);
 //   5. use columns only when some chunk is longer than W; W a multiple of 64,
 //      and of 64 KiB (>= 1 MiB) when automatic;
-//   6. number the segment descriptors of multi-column groups densely (nseg).
+//   6. number the segment descriptors of multi-column groups densely (nseg);
+// and the multi-GPU split (plan_shards) must give contiguous shards, on
+// k = min(#GPUs, ceil(bytes / shard_bytes)) GPUs, each within one chunk of an
+// equal share of the bytes.
 // Prints "plan ok <cases>" and exits 0, or the first violation and exits 1.
 #include <stdio.h>
 #include <stdlib.h>
@@ -115,6 +118,36 @@ static void check(const std::vector<uint64_t>& len, uint64_t cap, uint64_t slice
         (unsigned long long)(P.nregions * P.region), (unsigned long long)cap);
 }
 
+static void check_shards(const std::vector<uint64_t>& len, size_t ndev, uint64_t per,
+                         const char* what) {
+  size_t k = 0;
+  const std::vector<uint32_t> sh = plan_shards(len, ndev, per, &k);
+  uint64_t total = 0, longest = 0;
+  for (uint64_t L : len) total += L, longest = std::max(longest, L);
+  const size_t want_k = (size_t)std::min<uint64_t>(std::max<size_t>(1, ndev),
+                                                   std::max<uint64_t>(1, (total + per - 1) / per));
+  CHECK(k == want_k, "%s: %zu shards, want %zu", what, k, want_k);
+  CHECK(sh.size() == len.size(), "%s: shard list size", what);
+  std::vector<uint64_t> bytes(k, 0);
+  for (size_t i = 0; i < sh.size(); ++i) {
+    CHECK(sh[i] < k, "%s: shard %u >= %zu", what, sh[i], k);
+    // contiguous ranges; an index may be skipped when one chunk outweighs a share
+    if (i) CHECK(sh[i] >= sh[i - 1], "%s: shards not contiguous", what);
+    if (sh[i] < k) bytes[sh[i]] += len[i];
+  }
+  for (size_t d = 0; d < k; ++d)
+    CHECK(bytes[d] <= total / k + longest, "%s: shard %zu holds %llu of %llu B", what, d,
+          (unsigned long long)bytes[d], (unsigned long long)total);
+  bool equal = true;
+  for (uint64_t L : len) equal = equal && L == len.front();
+  if (equal && !len.empty()) {  // equal parts: every GPU that can get one does
+    size_t used = 0;
+    for (size_t d = 0; d < k; ++d) used += bytes[d] > 0;
+    CHECK(used == std::min(k, len.size()), "%s: %zu of %zu shards used for %zu equal parts", what,
+          used, k, len.size());
+  }
+}
+
 int main() {
   const uint64_t MiB = 1ull << 20, GiB = 1ull << 30;
   std::mt19937_64 rng(1234);
@@ -167,6 +200,20 @@ int main() {
     std::vector<uint64_t> v(1 + rng() % 300);
     for (auto& L : v) L = 1 + rng() % (1 + (rng() % 4 == 0 ? 200 * MiB : 3 * MiB));
     run(v, "random mix");
+  }
+  {  // multi-GPU split
+    std::vector<std::vector<uint64_t>> sets = {
+        {}, {1}, std::vector<uint64_t>(4096, 10 * MiB), std::vector<uint64_t>(10000, 10 * MiB),
+        std::vector<uint64_t>(3, 20 * GiB)};
+    std::vector<uint64_t> mix;
+    for (int i = 0; i < 5000; ++i) mix.push_back(1 + rng() % (64 * MiB));
+    sets.push_back(mix);
+    for (const auto& v : sets)
+      for (size_t nd : {(size_t)1, (size_t)2, (size_t)3, (size_t)8})
+        for (uint64_t per : {(uint64_t)1, 1 * GiB, 4 * GiB, 64 * GiB}) {
+          check_shards(v, nd, per, "shards");
+          ++cases;
+        }
   }
   printf("plan %s %d cases\n", fails ? "FAIL" : "ok", cases);
   return fails ? 1 : 0;
