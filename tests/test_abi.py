@@ -144,6 +144,19 @@ def test_plan_parts_range_begin_and_capacity():
     assert L.qsmd5_plan_parts(5, 0, 0, 0, 0, None, 0, ctypes.byref(need)) == -errno.EINVAL
 
 
+def test_kernel_choice_policy_host_only(monkeypatch):
+    """The kernel selection is host logic (no GPU): latency kernel up to 16 384
+    chunks, its 64 KiB-ring form up to 32 768, then the coalesced kernel for
+    16-B-aligned chunks or the one-wave kernel; QSMD5_KERNEL overrides."""
+    monkeypatch.delenv("QSMD5_KERNEL", raising=False)
+    A = qsmd5.FLAG_ALIGNED16
+    assert [qsmd5.kernel_choice(n) for n in (1, 512, 16384, 16385, 32768, 32769)] == [1, 1, 1, 3, 3, 0]
+    assert qsmd5.kernel_choice(32769, A) == 2 and qsmd5.kernel_choice(512, A) == 1
+    for name, want, want_aligned in (("pc", 1, 1), ("pc2", 3, 3), ("v1", 0, 0), ("coal", 0, 2)):
+        monkeypatch.setenv("QSMD5_KERNEL", name)
+        assert qsmd5.kernel_choice(100) == want and qsmd5.kernel_choice(100, A) == want_aligned
+
+
 def test_strerror():
     L = qsmd5.lib()
     assert L.qsmd5_strerror(0) == b"success"
