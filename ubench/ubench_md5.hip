@@ -755,6 +755,13 @@ int main(int argc, char** argv) {
     run_md5(512, 32ull << 20, 2, false, 0, 4096);
     return 0;
   }
+  if (!strcmp(mode, "fp_pmc")) {
+    // one launch each under rocprofv3 --pmc: dense 10 MiB, strided 10 MiB, strided 64 MiB
+    run_md5(512, 10ull << 20, 1, false, 1, 0);
+    run_md5(512, 10ull << 20, 1, false, 1, (54ull << 20) + 4096);
+    run_md5(512, 64ull << 20, 1, false, 1, 4096);
+    return 0;
+  }
   if (!strcmp(mode, "footprint")) {
     // 10 MiB chunks dense vs spread at a 32/64 MiB + 4 KiB stride; 10 000 dense
     // chunks (98 GiB footprint).  A two-producer-wave variant of the latency
