@@ -195,6 +195,17 @@ static double run_issue(ukern k, int instr_per_iter, int iters, int threads) {
 static bool g_host_pinned = false;  // "zc" mode: chunks in pinned host memory (zero-copy)
 static uint32_t g_skew = kPcSkewBlocks;  // latency kernel start skew (blocks per lane)
 
+// lane order: 0 chunk i; 1 lane l of wave w gets chunk l * (B/64) + w; 2 random
+// permutation inside each group of 64; 3 random permutation of all chunks
+// lane order: 0 chunk i; 1 lane l of wave w gets chunk l * (B/64) + w; 2 random
+// permutation inside each group of 64; 3 random permutation of all chunks
+template <int kPerm, uint32_t kMin>
+__global__ __launch_bounds__(128) void k_pc_perm(const ChunkDesc* __restrict__ chunks,
+                                                 const uint32_t* __restrict__ order, uint32_t n,
+                                                 uint32_t* __restrict__ digests, uint32_t skew) {
+  pc_body<false, 1, kPcHalf, kPerm, kMin>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
+}
+static int g_interleave = 0;
 static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint64_t pad = 0) {
   uint64_t stride = ((L + 255) & ~uint64_t(255)) + pad;
   uint8_t* d_data;
@@ -210,6 +221,18 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   for (int i = 0; i < B; ++i) {
     h[i].ptr = d_data + stride * (uint64_t)i;
     h[i].len = L;
+  }
+  if (g_interleave) {
+    std::vector<ChunkDesc> p(h);
+    uint64_t x = 88172645463325252ull;
+    auto rnd = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+    if (g_interleave == 1 && B % 64 == 0)
+      for (int i = 0; i < B; ++i) p[i] = h[(uint64_t)(i % 64) * (B / 64) + i / 64];
+    const int grp = g_interleave == 2 ? 64 : B;
+    if (g_interleave >= 2)
+      for (int g0 = 0; g0 < B; g0 += grp)
+        for (int i = std::min(B, g0 + grp) - 1; i > g0; --i) std::swap(p[i], p[g0 + rnd() % (i - g0 + 1)]);
+    h = p;
   }
   ChunkDesc* d_desc;
   uint32_t* d_dig;
@@ -262,12 +285,12 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   med = s[s.size() / 2];
   double gib = (double)L * B / (1u << 30);
   if (pad) printf("(stride pad %llu) ", (unsigned long long)pad);
-  if ((which == 1 || which == 3 || which == 4 || which == 5 || which == 7) && g_skew)
+  if ((which == 1 || which == 3 || which == 4 || which == 5) && g_skew)
     printf("(skew %u) ", g_skew);
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 7 ? "pc-p2" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -753,6 +776,25 @@ int main(int argc, char** argv) {
     }
     run_md5(512, 32ull << 20, 2, false, 0, 0);
     run_md5(512, 32ull << 20, 2, false, 0, 4096);
+    return 0;
+  }
+  if (!strcmp(mode, "span")) {
+    // same footprint, different lane->chunk maps: per-wave address span vs stride
+    static const char* names[] = {"in order", "interleaved", "shuffled in 64s", "shuffled all"};
+    for (uint64_t pad : {(uint64_t)0, (uint64_t)4352})
+      for (int m = 0; m < 4; ++m) {
+        g_interleave = m;
+        printf("(%s, pad %llu) ", names[m], (unsigned long long)pad);
+        run_md5(512, 10ull << 20, 2, false, 1, pad);
+      }
+    for (uint64_t L : {32ull << 20, 64ull << 20})
+      for (uint64_t pad : {(uint64_t)0, (uint64_t)4352})
+        for (int m : {0, 2, 3}) {
+          g_interleave = m;
+          printf("(%s, pad %llu) ", names[m], (unsigned long long)pad);
+          run_md5(512, L, 1, false, 1, pad);
+        }
+    g_interleave = 0;
     return 0;
   }
   if (!strcmp(mode, "fp_pmc")) {
