@@ -241,6 +241,33 @@ def config5(reps, n=10000):
     del t
 
 
+def pool(reps, n=512):
+    """Pooled part buffers handed out in any order: n x 10 MiB device buffers cut
+    from one allocation at an exact 10 MiB stride, passed to qsmd5_hash_batch in
+    pool order and in a shuffled order (a buffer pool's free list).  The runtime
+    orders equal-length lanes by address, so both run at the same rate."""
+    import random
+    import torch
+    import qsmd5
+    L = 10 * MiB
+    g = gold("batch_10MiB.json")["md5"][:n]
+    t = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    qsmd5.synth_fill_lcg(t.data_ptr(), L, L, 12345, n, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    perm = list(range(n))
+    random.Random(5).shuffle(perm)
+    res = {}
+    for name, order in (("pool order", list(range(n))), ("shuffled", perm)):
+        chunks = [(t.data_ptr() + i * L, L) for i in order]
+        dt, digs = timed(lambda: qsmd5.hash_batch(chunks), reps)
+        ok = [d.hex() for d in digs] == [g[i] for i in order]
+        res[name] = {"GiBps": round(n * L / GiB / dt, 3), "ms": round(dt * 1e3, 3),
+                     "parity": "ok" if ok else "FAIL"}
+    emit({"config": "pool", "workload": "%d x 10 MiB device buffers at an exact 10 MiB stride, "
+                                        "synchronous qsmd5_hash_batch" % n, "results": res})
+    del t
+
+
 def saturation(reps, L=64 * 1024):
     """Throughput regime: 131072 independent chains (one wave per 64, 8 waves per
     CU = one resident round), where the coalesced kernel runs instead of the
@@ -309,6 +336,8 @@ def main():
             config4(args.reps)
         elif c == "5":
             config5(args.reps)
+        elif c == "pool":
+            pool(args.reps)
         elif c == "sat":
             saturation(args.reps)
             torch.cuda.empty_cache()
