@@ -117,8 +117,10 @@ QSMD5_API int qsmd5_hash_batch_ex(const qsmd5_chunk* chunks, size_t n, uint8_t (
 /* Device-resident fast path, asynchronous on `hip_stream` (a hipStream_t, or
  * NULL for the legacy default stream): d_chunks, d_order and d_digests are
  * device memory, every chunk ptr is device memory.  d_order (optional, may be
- * NULL) lists chunk indices in the order lanes take them; the host should pass
- * lengths sorted descending so the lanes of a wavefront finish together.
+ * NULL) lists chunk indices in the order lanes take them.  For speed, sort by
+ * length, descending, so that the lanes of a wavefront finish together; break
+ * ties by address, so that neighbouring buffers share a wavefront and spread
+ * over the HBM channels.  qsmd5_hash_batch does both itself.
  * Only enqueues work; the caller synchronises the stream. */
 QSMD5_API int qsmd5_hash_batch_device_async(const qsmd5_chunk* d_chunks, const uint32_t* d_order, size_t n,
                                   uint8_t (*d_digests)[16], void* hip_stream);
