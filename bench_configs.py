@@ -268,7 +268,7 @@ def pool(reps, n=512):
     del t
 
 
-def saturation(reps, L=64 * 1024):
+def saturation(reps, L=64 * 1024, pad=4352):
     """Throughput regime: 131072 independent chains (one wave per 64, 8 waves per
     CU = one resident round), where the coalesced kernel runs instead of the
     latency kernel.  Reports the median and best of >= 10 launches."""
@@ -276,7 +276,7 @@ def saturation(reps, L=64 * 1024):
     import qsmd5
     from oracle_util import md5_many
     n = 131072
-    S = L + 4352  # skewed stride: lanes walk in lockstep, avoid one-channel strides
+    S = L + pad  # skewed stride: lanes walk in lockstep, avoid one-channel strides
     t = torch.empty(n * S, dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream()
     qsmd5.synth_fill_lcg(t.data_ptr(), S, L, 5, n, s.cuda_stream)
@@ -301,8 +301,8 @@ def saturation(reps, L=64 * 1024):
     want = md5_many([(host.ctypes.data + i * S, L) for i in range(64)])
     ok = [bytes(r) for r in dig[:64].cpu().numpy()] == want
     gbs = n * L / (med * 1e-3) / 1e9
-    emit({"config": "saturation", "workload": "%d x %d KiB device-resident, stride +4352 B (kernel %s)" % (
-        n, L // 1024, ["v1", "pc", "coal", "pc2"][qsmd5.kernel_choice(n, qsmd5.FLAG_ALIGNED16)]),
+    emit({"config": "saturation", "workload": "%d x %d KiB device-resident, stride +%d B (kernel %s)" % (
+        n, L // 1024, pad, ["v1", "pc", "coal", "pc2"][qsmd5.kernel_choice(n, qsmd5.FLAG_ALIGNED16)]),
         "GiBps": round(n * L / GiB / (med * 1e-3), 1), "GBps": round(gbs, 1),
         "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "kernel_ms_median": round(med, 3),
         "kernel_ms_best": round(best, 3), "launches": reps,
@@ -336,6 +336,11 @@ def main():
             config4(args.reps)
         elif c == "5":
             config5(args.reps)
+        elif c == "satpad":  # exact power-of-two strides vs the padded default
+            for L in (64 * 1024, 256 * 1024):
+                for pad in (0, 4352):
+                    saturation(args.reps, L=L, pad=pad)
+                    torch.cuda.empty_cache()
         elif c == "pool":
             pool(args.reps)
         elif c == "sat":
