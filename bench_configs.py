@@ -148,37 +148,49 @@ def many_small(reps, n=1 << 20, L=1024):
     """Many small objects (qsfs uploads every file below 20 MiB as one PutObject
     with its own Content-MD5, QSClient.cpp:437-458): n chunks of L bytes in one
     host buffer, one batch.  Reports the wall time and the kernel window, so the
-    host-side cost per chunk (classification, sort, descriptors) is visible."""
+    host-side cost per chunk (classification, sort, descriptors) is visible.
+    Run for pageable host memory with and without QSMD5_FLAG_HOST (the caller
+    vouches that every chunk is host memory: no per-chunk pointer query), and
+    for pinned host memory (the runtime's range cache answers after one query)."""
     import numpy as np
     import qsmd5
     from oracle_util import md5_many
-    host = np.empty(n * L, dtype=np.uint8)
-    rng = np.random.default_rng(5)
-    host[:] = rng.integers(0, 256, size=n * L, dtype=np.uint8)
-    desc = np.empty((n, 2), dtype=np.uint64)
-    desc[:, 0] = host.ctypes.data + np.arange(n, dtype=np.uint64) * L
-    desc[:, 1] = L
-    out = np.empty((n, 16), dtype=np.uint8)
     Lb = qsmd5.lib()
+    for mem, flags in (("pageable", 0), ("pageable", qsmd5.FLAG_HOST), ("pinned", 0)):
+        if mem == "pinned":
+            pp = qsmd5.alloc_pinned(n * L)
+            host = np.ctypeslib.as_array((ctypes.c_uint8 * (n * L)).from_address(pp))
+        else:
+            host = np.empty(n * L, dtype=np.uint8)
+        rng = np.random.default_rng(5)
+        host[:] = rng.integers(0, 256, size=n * L, dtype=np.uint8)
+        desc = np.empty((n, 2), dtype=np.uint64)
+        desc[:, 0] = host.ctypes.data + np.arange(n, dtype=np.uint64) * L
+        desc[:, 1] = L
+        out = np.empty((n, 16), dtype=np.uint8)
 
-    def run():
-        rc = Lb.qsmd5_hash_batch_ex(ctypes.cast(desc.ctypes.data, ctypes.POINTER(qsmd5.qsmd5_chunk)),
-                                    n, ctypes.cast(out.ctypes.data, ctypes.POINTER(ctypes.c_uint8)), 0)
-        assert rc == 0, rc
-        return out
+        def run():
+            rc = Lb.qsmd5_hash_batch_ex(
+                ctypes.cast(desc.ctypes.data, ctypes.POINTER(qsmd5.qsmd5_chunk)), n,
+                ctypes.cast(out.ctypes.data, ctypes.POINTER(ctypes.c_uint8)), flags)
+            assert rc == 0, rc
+            return out
 
-    dt, _ = timed(run, reps)
-    wall, kern = qsmd5.last_timing()
-    sample = list(range(0, n, n // 64))
-    want = md5_many([(host.ctypes.data + i * L, L) for i in sample])
-    ok = [bytes(out[i]) for i in sample] == want
-    emit({"config": "many-small", "workload": "%d x %d B objects in one pageable host buffer, one batch"
-                                             % (n, L),
-          "objects_per_s": round(n / dt), "GiBps": round(n * L / GiB / dt, 3),
-          "seconds": round(dt, 4), "last_call_wall_ms": round(wall, 2),
-          "last_call_kernel_window_ms": round(kern, 2),
-          "host_us_per_chunk": round((wall - kern) * 1e3 / n, 3),
-          "parity": "ok (64 sampled vs oracle)" if ok else "FAIL"})
+        dt, _ = timed(run, reps)
+        wall, kern = qsmd5.last_timing()
+        sample = list(range(0, n, n // 64))
+        want = md5_many([(host.ctypes.data + i * L, L) for i in sample])
+        ok = [bytes(out[i]) for i in sample] == want
+        emit({"config": "many-small", "workload": "%d x %d B objects in one %s host buffer, one batch%s"
+                                                 % (n, L, mem, ", QSMD5_FLAG_HOST" if flags else ""),
+              "objects_per_s": round(n / dt), "GiBps": round(n * L / GiB / dt, 3),
+              "seconds": round(dt, 4), "last_call_wall_ms": round(wall, 2),
+              "last_call_kernel_window_ms": round(kern, 2),
+              "host_us_per_chunk": round((wall - kern) * 1e3 / n, 3),
+              "parity": "ok (64 sampled vs oracle)" if ok else "FAIL"})
+        del host
+        if mem == "pinned":
+            qsmd5.free_pinned(pp)
 
 
 def config4(reps):

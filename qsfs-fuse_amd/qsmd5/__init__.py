@@ -20,7 +20,7 @@ __all__ = [
     "Md5Error", "lib", "lib_path", "hexdigest", "md5", "md5_stream", "MD5", "hash_batch",
     "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
     "alloc_pinned", "free_pinned", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
-    "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16",
+    "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -143,6 +143,7 @@ def kernel_choice(n, flags=0):
 
 FLAG_REF_TRUNCATE32 = 1
 FLAG_ALIGNED16 = 2
+FLAG_HOST = 4  # every chunk is host memory: skip the per-chunk pointer query
 
 
 def hexdigest(digest):

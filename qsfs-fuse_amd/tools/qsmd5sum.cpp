@@ -115,8 +115,9 @@ int main(int argc, char** argv) {
   }
   std::vector<uint8_t> dig(16 * chunks.size());
   if (rc == 0 && !chunks.empty()) {
-    int e = qsmd5_hash_batch(chunks.data(), chunks.size(),
-                             reinterpret_cast<uint8_t(*)[16]>(dig.data()));
+    // the files were read into host memory: no per-part pointer query
+    int e = qsmd5_hash_batch_ex(chunks.data(), chunks.size(),
+                                reinterpret_cast<uint8_t(*)[16]>(dig.data()), QSMD5_FLAG_HOST);
     if (e != 0) {
       fprintf(stderr, "qsmd5sum: GPU hashing failed: %s (%s)\n", qsmd5_strerror(e),
               qsmd5_last_error());

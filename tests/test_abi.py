@@ -50,6 +50,18 @@ def test_library_exports_every_declared_symbol():
     assert not [s for s in exported if "device_stub" in s or "launch_" in s]
 
 
+def test_flags_match_header():
+    """The binding's FLAG_* constants are the header's QSMD5_FLAG_* values."""
+    text = open(os.path.join(ROOT, "include", "qsmd5.h")).read()
+    flags = dict(re.findall(r"#define QSMD5_FLAG_(\w+)\s+(\d+)", text))
+    assert set(flags) >= {"NONE", "REF_TRUNCATE32", "ALIGNED16", "HOST"}
+    for name, val in flags.items():
+        if name != "NONE":
+            assert getattr(qsmd5, "FLAG_" + name) == int(val), name
+    vals = [int(v) for k, v in flags.items() if k != "NONE"]
+    assert all(v & (v - 1) == 0 for v in vals) and len(set(vals)) == len(vals)  # distinct bits
+
+
 def test_abi_version():
     assert qsmd5.lib().qsmd5_abi_version() == 1
 

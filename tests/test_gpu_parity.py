@@ -216,6 +216,50 @@ def test_pool_buffers_in_any_order(golden):
     del t
 
 
+def test_classifier_many_allocations_and_host_flag():
+    """The runtime remembers the exact range of each HIP allocation it has seen
+    (8 ranges).  Here more device and pinned allocations than that are mixed with
+    pageable buffers in shuffled order.  Chunks end on an allocation's last
+    byte.  Every chunk must still be classified right.  QSMD5_FLAG_HOST on the
+    host-only subset gives the same digests without the pointer queries."""
+    import random
+    rng = random.Random(11)
+    items, keep = [], []
+    for i in range(10):  # pinned: distinct hipHostMalloc ranges
+        L = 65536 + 37 * i
+        p = qsmd5.alloc_pinned(L)
+        keep.append(p)
+        data = bytes(lcg_bytes(900 + i, L))
+        ctypes.memmove(p, data, L)
+        items += [("host", (p, L), md5_ref(data)), ("host", (p + L - 1000, 1000), md5_ref(data[-1000:]))]
+    tensors = []
+    for i in range(12):  # device: >= 10 MiB each, so torch gives each its own hipMalloc
+        L = (10 << 20) + 4097 * i
+        t = dev_lcg(950 + i, L)
+        tensors.append(t)
+        data = t.cpu().numpy().tobytes()
+        items += [("dev", (t.data_ptr(), L), md5_ref(data)),
+                  ("dev", (t.data_ptr() + L - 777, 777), md5_ref(data[-777:]))]
+    pageable = []
+    for i in range(5):
+        L = 300000 + 11 * i
+        b = lcg_bytes(990 + i, L)
+        pageable.append(b)
+        items.append(("host", (ctypes.addressof(b), L), md5_ref(bytes(b))))
+    items.append(("host", (0, 0), md5_ref(b"")))
+    try:
+        for rnd in range(2):
+            rng.shuffle(items)
+            got = qsmd5.hash_batch([c for _, c, _ in items])
+            assert got == [w for _, _, w in items], rnd
+        host = [(c, w) for k, c, w in items if k == "host"]
+        got = qsmd5.hash_batch([c for c, _ in host], flags=qsmd5.FLAG_HOST)
+        assert got == [w for _, w in host]
+    finally:
+        for p in keep:
+            qsmd5.free_pinned(p)
+
+
 def test_batch_pinned_host(golden):
     g = golden("batch_10MiB.json")
     n, L = 96, g["len"]
