@@ -280,14 +280,13 @@ def pool(reps, n=512):
     del t
 
 
-def saturation(reps, L=64 * 1024, pad=4352):
+def saturation(reps, L=64 * 1024, pad=4352, n=131072):
     """Throughput regime: 131072 independent chains (one wave per 64, 8 waves per
     CU = one resident round), where the coalesced kernel runs instead of the
     latency kernel.  Reports the median and best of >= 10 launches."""
     import torch
     import qsmd5
     from oracle_util import md5_many
-    n = 131072
     S = L + pad  # skewed stride: lanes walk in lockstep, avoid one-channel strides
     t = torch.empty(n * S, dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream()
@@ -353,6 +352,10 @@ def main():
                 for pad in (0, 4352):
                     saturation(args.reps, L=L, pad=pad)
                     torch.cuda.empty_cache()
+        elif c == "tiny":  # device-resident tiny chunks: the per-chain fixed cost
+            for L, n in ((1024, 1 << 20), (4096, 1 << 20), (16384, 1 << 19)):
+                saturation(args.reps, L=L, pad=0, n=n)
+                torch.cuda.empty_cache()
         elif c == "pool":
             pool(args.reps)
         elif c == "sat":
