@@ -275,25 +275,31 @@ MemKind classify(const void* p, int* owner = nullptr, bool* hip_known = nullptr)
     (void)hipGetLastError();  // pageable host memory: clear the sticky error
     return kHostMem;
   }
-  if (hip_known) *hip_known = true;
+  // pageable memory either fails the query or reports "unregistered"
+  if (hip_known) *hip_known = a.type != hipMemoryTypeUnregistered;
   if (a.type != hipMemoryTypeDevice) return kHostMem;
   if (owner) *owner = a.device;
   return kDeviceMem;
 }
 
 // Classifies the chunk pointers of one batch.  The query above costs ~30 ns
-// for HIP memory and ~70 ns for pageable memory.  It is serialised inside HIP,
-// so host threads make it slower, not faster (profiles/r01_ubench_classify.log).
-// A HIP allocation (device or pinned host) found once is remembered by its
-// exact range (hipMemGetAddressRange).  Later chunks inside that range need no
-// query: every byte of one allocation has the same kind and owner.  This is not
-// a guess about neighbours.  A batch's chunks mostly sit in a few allocations
-// (a pool, a file buffer, torch's caching allocator).  Pageable memory has no
-// range to remember and is queried per pointer.  QSMD5_FLAG_HOST skips the
-// query altogether.
+// for HIP memory and 70-260 ns for pageable memory.  It is serialised inside
+// HIP, so host threads make it slower, not faster
+// (profiles/r01_ubench_classify.log).  Two exact range caches avoid it:
+// - A HIP allocation (device, pinned or registered host) found once is
+//   remembered by its exact range (hipMemGetAddressRange).  Every byte of one
+//   allocation has the same kind and owner.
+// - A pointer HIP does not know (pageable) is remembered by the VMA that holds
+//   it (/proc/self/maps, read once per batch), if that VMA is readable and
+//   anonymous or a regular file.  Device memory never lives in such a VMA:
+//   VRAM is an unreadable reservation or a mapping of a /dev file, and VMAs of
+//   different backing or permissions never merge.  This cache only ever
+//   answers "host", so it can never send a host pointer to a kernel.
+// A batch's chunks mostly sit in a few allocations (a pool, a file buffer,
+// torch's caching allocator).  QSMD5_FLAG_HOST skips all queries.
 class Classifier {
  public:
-  explicit Classifier(int flags) : all_host_(flags & QSMD5_FLAG_HOST) {}
+  Classifier(int flags, size_t n) : all_host_(flags & QSMD5_FLAG_HOST), use_maps_(n >= kMapsMinChunks) {}
   MemKind operator()(const void* p, int* owner) {
     *owner = -1;
     if (all_host_ || !p) return kHostMem;
@@ -311,18 +317,54 @@ class Classifier {
       hipDeviceptr_t base = nullptr;
       size_t size = 0;
       if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) == hipSuccess && size &&
-          a - reinterpret_cast<uintptr_t>(base) < size) {
-        ranges_[next_] = Range{reinterpret_cast<uintptr_t>(base), size, kind, *owner};
-        next_ = (next_ + 1) % kRanges;
-        used_ = used_ < kRanges ? used_ + 1 : kRanges;
-      } else {
+          a - reinterpret_cast<uintptr_t>(base) < size)
+        remember(reinterpret_cast<uintptr_t>(base), size, kind, *owner);
+      else
         (void)hipGetLastError();
-      }
+    } else if (use_maps_ && kind == kHostMem) {
+      if (!maps_read_) read_maps();
+      auto it = std::upper_bound(vmas_.begin(), vmas_.end(), a,
+                                 [](uintptr_t x, const Vma& v) { return x < v.lo; });
+      if (it != vmas_.begin() && a - (it - 1)->lo < (it - 1)->hi - (it - 1)->lo)
+        remember((it - 1)->lo, (it - 1)->hi - (it - 1)->lo, kHostMem, -1);
     }
     return kind;
   }
 
  private:
+  static constexpr size_t kMapsMinChunks = 256;  // below this, queries are cheaper than a parse
+  struct Vma {
+    uintptr_t lo, hi;
+  };
+  void remember(uintptr_t lo, size_t size, MemKind kind, int owner) {
+    ranges_[next_] = Range{lo, size, kind, owner};
+    next_ = (next_ + 1) % kRanges;
+    used_ = used_ < kRanges ? used_ + 1 : kRanges;
+  }
+  // Readable VMAs that are anonymous, [heap]/[stack]/[anon:...], or regular
+  // files outside /dev; anything else (device files, dma-bufs, anon inodes)
+  // is left to the per-pointer query.
+  void read_maps() {
+    maps_read_ = true;
+    FILE* f = fopen("/proc/self/maps", "r");
+    if (!f) return;
+    char line[4096];
+    while (fgets(line, sizeof(line), f)) {
+      unsigned long long lo = 0, hi = 0;
+      char perms[8] = {0};
+      int path_at = 0;
+      if (sscanf(line, "%llx-%llx %7s %*s %*s %*s %n", &lo, &hi, perms, &path_at) < 3) continue;
+      if (perms[0] != 'r' || hi <= lo) continue;
+      const char* path = line + path_at;
+      while (*path == ' ') ++path;
+      const bool anon = *path == '\n' || *path == 0;
+      const bool special = *path == '[' && (!strncmp(path, "[heap]", 6) || !strncmp(path, "[stack]", 7) ||
+                                           !strncmp(path, "[anon:", 6));
+      const bool file = *path == '/' && strncmp(path, "/dev/", 5) != 0;
+      if (anon || special || file) vmas_.push_back(Vma{(uintptr_t)lo, (uintptr_t)hi});
+    }
+    fclose(f);
+  }
   struct Range {
     uintptr_t lo;
     size_t size;
@@ -333,6 +375,9 @@ class Classifier {
   Range ranges_[kRanges] = {};
   int used_ = 0, next_ = 0;
   bool all_host_;
+  bool use_maps_;
+  bool maps_read_ = false;
+  std::vector<Vma> vmas_;  // sorted: /proc/self/maps lists VMAs in address order
 };
 
 int kernel_choice(size_t n, bool aligned16) {
@@ -366,7 +411,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
 
   std::vector<uint64_t> len(n);
   std::vector<MemKind> kind(n);
-  Classifier cls(flags);
+  Classifier cls(flags, n);
   for (size_t i = 0; i < n; ++i) {
     uint64_t L = chunks[i].len;
     if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;
@@ -650,7 +695,7 @@ int run_sharded(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
   std::vector<std::vector<uint32_t>> part(nd);
   std::vector<uint32_t> host;
   if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
-  Classifier cls(flags);
+  Classifier cls(flags, n);
   for (size_t i = 0; i < n; ++i) {
     uint64_t L = chunks[i].len;
     if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;

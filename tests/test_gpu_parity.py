@@ -217,11 +217,13 @@ def test_pool_buffers_in_any_order(golden):
 
 
 def test_classifier_many_allocations_and_host_flag():
-    """The runtime remembers the exact range of each HIP allocation it has seen
-    (8 ranges).  Here more device and pinned allocations than that are mixed with
-    pageable buffers in shuffled order.  Chunks end on an allocation's last
-    byte.  Every chunk must still be classified right.  QSMD5_FLAG_HOST on the
-    host-only subset gives the same digests without the pointer queries."""
+    """The runtime remembers the exact range of each HIP allocation it has seen,
+    and the VMA of each pageable pointer (8 ranges in all).  Here more device
+    and pinned allocations than that are mixed with pageable buffers in shuffled
+    order, over 256 chunks so the VMA cache is on.  Chunks end on an
+    allocation's last byte.  Every chunk must still be classified right.
+    QSMD5_FLAG_HOST on the host-only subset gives the same digests without the
+    pointer queries."""
     import random
     rng = random.Random(11)
     items, keep = [], []
@@ -247,6 +249,17 @@ def test_classifier_many_allocations_and_host_flag():
         pageable.append(b)
         items.append(("host", (ctypes.addressof(b), L), md5_ref(bytes(b))))
     items.append(("host", (0, 0), md5_ref(b"")))
+    # > 256 chunks, so the runtime also reads /proc/self/maps and remembers the
+    # VMAs of pageable pointers: slices of the pageable and device buffers
+    for j in range(300):
+        b = pageable[j % 5]
+        off = (j * 997) % (len(b) - 2000)
+        items.append(("host", (ctypes.addressof(b) + off, 1500), md5_ref(bytes(b)[off:off + 1500])))
+    for j in range(60):
+        t = tensors[j % 12]
+        off = (j * 65537) % (t.numel() - 5000)
+        items.append(("dev", (t.data_ptr() + off, 4000),
+                      md5_ref(t[off:off + 4000].cpu().numpy().tobytes())))
     try:
         for rnd in range(2):
             rng.shuffle(items)
