@@ -85,9 +85,9 @@ typedef struct qsmd5_part {
 #define QSMD5_FLAG_ALIGNED16 2      /* device_async_ex: caller promises 16-B-aligned chunk ptrs */
 #define QSMD5_FLAG_HOST 4           /* hash_batch_ex: caller promises every chunk is host memory
                                      * (pageable, pinned or registered), as qsfs's part buffers
-                                     * are; skips the per-chunk pointer query (~70 ns per pageable
-                                     * chunk).  A device pointer in such a batch is a caller bug:
-                                     * the H2D copy then fails or reads the wrong memory. */
+                                     * are; skips pointer classification (otherwise one query per
+                                     * new allocation or VMA, cached by range).  A device pointer
+                                     * in such a batch is a caller bug: the H2D copy then fails. */
 
 /* Initialise the runtime on the current HIP device, or on the QSMD5_DEVICES
  * list (idempotent).  Returns 0, -ENODEV when no GPU is usable or the list
