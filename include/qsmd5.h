@@ -87,7 +87,7 @@ typedef struct qsmd5_part {
                                      * (pageable, pinned or registered), as qsfs's part buffers
                                      * are; skips pointer classification (otherwise one query per
                                      * new allocation or VMA, cached by range).  A device pointer
-                                     * in such a batch is a caller bug: the H2D copy then fails. */
+                                     * in such a batch is a caller bug (it is staged as host). */
 
 /* Initialise the runtime on the current HIP device, or on the QSMD5_DEVICES
  * list (idempotent).  Returns 0, -ENODEV when no GPU is usable or the list
