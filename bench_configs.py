@@ -341,6 +341,10 @@ def main():
             many_small(args.reps)
         elif c == "5h":
             config3(args.reps, n=10000, label=" -- BASELINE config 5 host-resident (97.7 GiB)")
+        elif c == "3cmp":  # pinned vs pageable at equal sizes
+            for n in (1024, 4096):
+                config3(args.reps, n=n)
+                config3_pageable(args.reps, n=n)
         elif c == "3p":
             config3_pageable(args.reps)
         elif c == "4":
