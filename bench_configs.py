@@ -345,6 +345,9 @@ def main():
             for n in (1024, 4096):
                 config3(args.reps, n=n)
                 config3_pageable(args.reps, n=n)
+        elif c == "3cols":  # host batches across sizes, for column-width sweeps
+            for n in (64, 1024, 4096):
+                config3_pageable(args.reps, n=n)
         elif c == "3p":
             config3_pageable(args.reps)
         elif c == "4":

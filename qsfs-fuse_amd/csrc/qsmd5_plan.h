@@ -11,7 +11,7 @@
 // (group, column): one H2D transfer into a region, then one kernel launch that
 // resumes each chain from its parked state.  Columns let every chain start as
 // soon as the first column lands, so the serial chain of the LAST chunk copied
-// no longer trails the transfer: only its last column (~8 ms at W ~ 1 MiB)
+// no longer trails the transfer: only its last column (~2 ms at W = 256 KiB)
 // does.  W = kNoColumns (chunks no longer than a column) degenerates to
 // whole-chunk row slices.
 //
@@ -33,7 +33,9 @@ constexpr uint64_t kSliceMax = 4ull << 30;
 constexpr uint64_t kAlign = 256;
 constexpr uint64_t kSkew = 4096 + 256;
 constexpr uint64_t kColGrain = 64ull << 10;  // automatic column widths are multiples of this
-constexpr uint64_t kColMin = 1ull << 20;     // ... and at least this (>= 1 MiB per-chunk copies)
+constexpr uint64_t kColMin = 256ull << 10;   // ... and at least this: 2-D copies keep the link
+                                             // rate down to 256 KiB rows, and 128 KiB loses 2%
+constexpr uint64_t kColMaxPerChunk = 1024;   // automatic columns per chunk (launches per group)
 constexpr uint64_t kNoColumns = ~0ull;
 
 // Bytes one staged segment of L message bytes occupies in a region.
@@ -72,9 +74,12 @@ struct HostPlan {
 // staging_cap: bytes of device memory the ring may use.
 // slice_bytes: slice target, 0 = automatic (a quarter of the batch, clamped to
 //   [kSliceMin, kSliceMax]).
-// column_bytes: < 0 automatic (one column of every chunk fills about one
-//   slice; a multiple of kColGrain, at least kColMin); 0 = whole chunks;
-//   > 0 forced (rounded down to a multiple of 64, at least 64).
+// column_bytes: < 0 automatic: kColMin, or longest / kColMaxPerChunk for
+//   chunks over 256 MiB, a multiple of kColGrain.  Narrow columns shorten the
+//   tail: the chain of the last column starts only when its bytes have landed
+//   (1024 x 10 MiB pageable: 2.5 MiB columns 48.5 GiB/s, 256 KiB 52.4;
+//   profiles/r01_config3_column_width.jsonl).  0 = whole chunks; > 0 forced
+//   (rounded down to a multiple of 64, at least 64).
 inline HostPlan plan_host(const std::vector<uint64_t>& host_len, uint64_t staging_cap,
                           uint64_t slice_bytes, int64_t column_bytes) {
   HostPlan P;
@@ -86,9 +91,8 @@ inline HostPlan plan_host(const std::vector<uint64_t>& host_len, uint64_t stagin
       slice_bytes ? slice_bytes : std::min(kSliceMax, std::max(kSliceMin, host_total / 4));
   uint64_t w;
   if (column_bytes < 0) {
-    const uint64_t per = P.slice_target / host_len.size();
-    w = per > kSkew + kAlign ? (per - kSkew - kAlign) / kColGrain * kColGrain : 0;
-    w = std::max(w, kColMin);
+    const uint64_t per = (max_host + kColMaxPerChunk - 1) / kColMaxPerChunk;
+    w = std::max(kColMin, (per + kColGrain - 1) / kColGrain * kColGrain);
   } else if (column_bytes == 0) {
     w = kNoColumns;
   } else {

@@ -11,7 +11,8 @@
 //   4. fit every slice in one region, and the ring in the staging cap unless a
 //      single slice alone is larger (then one region of that size);
 //   5. use columns only when some chunk is longer than W; W a multiple of 64,
-//      and of 64 KiB (>= 1 MiB) when automatic;
+//      and when automatic a multiple of 64 KiB, >= kColMin, with at most
+//      kColMaxPerChunk (+1) columns per chunk;
 //   6. number the segment descriptors of multi-column groups densely (nseg);
 // and the multi-GPU split (plan_shards) must give contiguous shards, on
 // k = min(#GPUs, ceil(bytes / shard_bytes)) GPUs, each within one chunk of an
@@ -52,9 +53,12 @@ static void check(const std::vector<uint64_t>& len, uint64_t cap, uint64_t slice
   if (P.W != kNoColumns) {
     CHECK(P.W < longest, "%s: W %llu not below the longest chunk", what, (unsigned long long)P.W);
     CHECK(P.W % 64 == 0, "%s: W %llu not a multiple of 64", what, (unsigned long long)P.W);
-    if (col < 0)
+    if (col < 0) {
       CHECK(P.W % kColGrain == 0 && P.W >= kColMin, "%s: automatic W %llu", what,
             (unsigned long long)P.W);
+      CHECK((longest + P.W - 1) / P.W <= kColMaxPerChunk + 1, "%s: %llu columns per chunk", what,
+            (unsigned long long)((longest + P.W - 1) / P.W));
+    }
   } else {
     CHECK(col == 0 || (col < 0) || (uint64_t)std::max<int64_t>(64, col & ~63ll) >= longest,
           "%s: no columns although forced width %lld < longest", what, (long long)col);
