@@ -98,3 +98,21 @@ def test_bench_two_rank_rehearsal():
     assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 128
     assert r["parity"].startswith("ok: 128/128")
     assert r["cpu_baseline"] is None and r["scaling"] == "weak"
+
+
+def test_bench_rccl_path_world_one():
+    """The RCCL path of bench.py (nccl process group bound to the device,
+    all_gather_into_tensor of the digests, all_reduce MAX of the time) run at
+    world size 1 under torch.distributed.run: what every rank does on the
+    driver's 8-GPU node, minus the peers."""
+    cmd = [PY, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "2", "--warmup", "1",
+           "--batch", "64", "--dist-always", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, env=ENV, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 1 and r["config"]["global_batch"] == 64
+    assert r["parity"].startswith("ok: 64/64")
