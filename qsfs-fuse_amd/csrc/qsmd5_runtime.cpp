@@ -290,7 +290,8 @@ MemKind classify(const void* p, int* owner = nullptr, bool* hip_known = nullptr)
 //   remembered by its exact range (hipMemGetAddressRange).  Every byte of one
 //   allocation has the same kind and owner.
 // - A pointer HIP does not know (pageable) is remembered by the VMA that holds
-//   it (/proc/self/maps, read once per batch), if that VMA is readable and
+//   it (/proc/self/maps, read once per batch after QSMD5_MAPS_AFTER = 2048
+//   pageable queries), if that VMA is readable and
 //   anonymous or a regular file.  Device memory never lives in such a VMA:
 //   VRAM is an unreadable reservation or a mapping of a /dev file, and VMAs of
 //   different backing or permissions never merge.  This cache only ever
@@ -299,7 +300,9 @@ MemKind classify(const void* p, int* owner = nullptr, bool* hip_known = nullptr)
 // torch's caching allocator).  QSMD5_FLAG_HOST skips all queries.
 class Classifier {
  public:
-  Classifier(int flags, size_t n) : all_host_(flags & QSMD5_FLAG_HOST), use_maps_(n >= kMapsMinChunks) {}
+  Classifier(int flags, size_t n)
+      : all_host_(flags & QSMD5_FLAG_HOST),
+        maps_after_(n >= 2 ? env_u64("QSMD5_MAPS_AFTER", kMapsAfter) : ~0ull) {}
   MemKind operator()(const void* p, int* owner) {
     *owner = -1;
     if (all_host_ || !p) return kHostMem;
@@ -321,7 +324,7 @@ class Classifier {
         remember(reinterpret_cast<uintptr_t>(base), size, kind, *owner);
       else
         (void)hipGetLastError();
-    } else if (use_maps_ && kind == kHostMem) {
+    } else if (kind == kHostMem && ++pageable_queries_ >= maps_after_) {
       if (!maps_read_) read_maps();
       auto it = std::upper_bound(vmas_.begin(), vmas_.end(), a,
                                  [](uintptr_t x, const Vma& v) { return x < v.lo; });
@@ -332,7 +335,10 @@ class Classifier {
   }
 
  private:
-  static constexpr size_t kMapsMinChunks = 256;  // below this, queries are cheaper than a parse
+  // Parse the maps only after this many pageable queries in one batch: by then
+  // the queries have cost (70-260 ns each) about what one parse of a large
+  // process's maps does, so a batch never pays much more than twice the better.
+  static constexpr uint64_t kMapsAfter = 2048;
   struct Vma {
     uintptr_t lo, hi;
   };
@@ -375,7 +381,8 @@ class Classifier {
   Range ranges_[kRanges] = {};
   int used_ = 0, next_ = 0;
   bool all_host_;
-  bool use_maps_;
+  uint64_t maps_after_;
+  uint64_t pageable_queries_ = 0;
   bool maps_read_ = false;
   std::vector<Vma> vmas_;  // sorted: /proc/self/maps lists VMAs in address order
 };

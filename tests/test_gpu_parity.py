@@ -220,7 +220,7 @@ def test_classifier_many_allocations_and_host_flag():
     """The runtime remembers the exact range of each HIP allocation it has seen,
     and the VMA of each pageable pointer (8 ranges in all).  Here more device
     and pinned allocations than that are mixed with pageable buffers in shuffled
-    order, over 256 chunks so the VMA cache is on.  Chunks end on an
+    order, with the VMA cache on (QSMD5_MAPS_AFTER lowered) and off.  Chunks end on an
     allocation's last byte.  Every chunk must still be classified right.
     QSMD5_FLAG_HOST on the host-only subset gives the same digests without the
     pointer queries."""
@@ -249,8 +249,8 @@ def test_classifier_many_allocations_and_host_flag():
         pageable.append(b)
         items.append(("host", (ctypes.addressof(b), L), md5_ref(bytes(b))))
     items.append(("host", (0, 0), md5_ref(b"")))
-    # > 256 chunks, so the runtime also reads /proc/self/maps and remembers the
-    # VMAs of pageable pointers: slices of the pageable and device buffers
+    # many pageable chunks: with QSMD5_MAPS_AFTER lowered below, the runtime
+    # also reads /proc/self/maps and remembers the VMAs of pageable pointers
     for j in range(300):
         b = pageable[j % 5]
         off = (j * 997) % (len(b) - 2000)
@@ -261,7 +261,11 @@ def test_classifier_many_allocations_and_host_flag():
         items.append(("dev", (t.data_ptr() + off, 4000),
                       md5_ref(t[off:off + 4000].cpu().numpy().tobytes())))
     try:
-        for rnd in range(2):
+        for rnd, after in enumerate(("16", "16", None)):
+            if after:
+                os.environ["QSMD5_MAPS_AFTER"] = after
+            else:
+                os.environ.pop("QSMD5_MAPS_AFTER", None)
             rng.shuffle(items)
             got = qsmd5.hash_batch([c for _, c, _ in items])
             assert got == [w for _, _, w in items], rnd
@@ -269,6 +273,7 @@ def test_classifier_many_allocations_and_host_flag():
         got = qsmd5.hash_batch([c for c, _ in host], flags=qsmd5.FLAG_HOST)
         assert got == [w for _, w in host]
     finally:
+        os.environ.pop("QSMD5_MAPS_AFTER", None)
         for p in keep:
             qsmd5.free_pinned(p)
 
