@@ -192,6 +192,8 @@ __device__ __forceinline__ void lds_barrier() {
 // serial part: 4 VALU per step plus one ds_read_b128 per 4 steps.  The two waves
 // sit on different SIMDs, so the chain wave's issue slots are not shared.
 constexpr int kPcHalf = 4;  // blocks per ring half (one phase): 8 x 16 KiB = 128 KiB of LDS
+// s_waitcnt immediate (gfx9 encoding) for lgkmcnt(0) alone: vmcnt 63, expcnt 7.
+constexpr int kLgkmcnt0 = 0xC07F;
 
 struct PcBlockRegs {
   u32x4 q[4];
@@ -254,7 +256,15 @@ __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*rin
   read_slot(a, s0);
 #pragma unroll
   for (int h = 0; h < kHalf; ++h) {
+    // One wait per block: the operands of block h (read a whole block ago)
+    // are complete, then the 16 reads of block h+1 go out and the 256 VALU of
+    // block h need no wait at all.  Left to itself the compiler hoists two
+    // blocks of reads (32 > the 15 lgkmcnt can count) and then waits before
+    // every ds_read_b128's first use: 8 waits (issue slots) per block.
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
     if (h + 1 < kHalf) read_slot((h & 1) ? a : b, s0 + h + 1);
+    __builtin_amdgcn_sched_barrier(0);
     if (kAllLive || blk0 + (uint32_t)h < nblk) compress_slot((h & 1) ? b : a);  // blk0 may wrap (skew)
   }
 }
