@@ -130,6 +130,18 @@ inline HostPlan plan_host(const std::vector<uint64_t>& host_len, uint64_t stagin
       if (g.ncols > 1) P.nseg += act;
     }
   }
+  // Groups are formed; shrink the region to the largest slice actually
+  // planned, so that small batches get many regions and their copies run ahead
+  // of the kernels instead of waiting for the one region to free up (one
+  // 10 MiB part: 40 columns in 40 regions, not 1).
+  uint64_t need = 0;
+  for (const Slice& sl : P.slices) {
+    const Group& g = P.groups[sl.group];
+    uint64_t b = 0;
+    for (size_t k = 0; k < sl.active; ++k) b += stage_bytes(P.col_bytes(host_len[g.first + k], sl.col));
+    need = std::max(need, b);
+  }
+  P.region = std::max<uint64_t>(need, kAlign);
   const uint64_t cap = std::min<uint64_t>(staging_cap, host_total + P.region);
   P.nregions = (size_t)std::max<uint64_t>(1, cap / P.region);
   P.nregions = std::min(P.nregions, P.slices.size());
