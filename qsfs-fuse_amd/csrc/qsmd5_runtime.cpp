@@ -48,6 +48,7 @@ constexpr uint64_t kMaxChunkLen = 1ull << 38;
 constexpr int kComputeStreams = 8;
 constexpr int kMaxCopyStreams = 4;
 constexpr uint64_t kDefaultStaging = 16ull << 30;   // device staging ring
+constexpr uint64_t kInlineBytes = 256ull << 10;     // staged bytes a batch may carry inline
 
 
 thread_local std::string t_last_error;
@@ -143,8 +144,12 @@ struct Dev {
   hipStream_t copy[kMaxCopyStreams] = {};
   int ncopy = 2;  // H2D streams (QSMD5_COPY_STREAMS), slices alternate over them
   hipStream_t compute[kComputeStreams] = {};
-  DevBuf d_desc, d_order, d_dig, d_staging, d_state;
-  HostPinned h_desc, h_order, h_dig;
+  // d_meta / h_meta: one block [chunk + segment descriptors | lane orders |
+  // inline host data of tiny batches], so one H2D copy carries them all.
+  DevBuf d_meta, d_dig, d_staging, d_state;
+  HostPinned h_meta, h_dig;
+  // Per-batch events, reused (batches on one Dev are serialised by mu).
+  hipEvent_t ev_meta = nullptr, ev_first = nullptr, ev_last = nullptr;
   uint64_t staging_cap = kDefaultStaging;
   double last_wall_ms = 0, last_kernel_ms = 0;
 };
@@ -214,6 +219,10 @@ int init_dev(Dev& d, int device) {
     if ((e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
       return hip_fail(e, "hipStreamCreate");
   d.staging_cap = env_u64("QSMD5_STAGING_BYTES", kDefaultStaging);
+  if ((e = hipEventCreateWithFlags(&d.ev_meta, hipEventDisableTiming)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&d.ev_first, hipEventDefault)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&d.ev_last, hipEventDefault)) != hipSuccess)
+    return hip_fail(e, "hipEventCreate");
   return 0;
 }
 
@@ -471,27 +480,45 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   const std::vector<qsmd5::Slice>& slices = plan.slices;
   const size_t nseg = plan.nseg, nregions = plan.nregions;
   auto col_bytes = [&](uint64_t L, uint32_t j) { return plan.col_bytes(L, j); };
-  if (!slices.empty())
+  // Tiny host batches ride inline: the CPU copies their bytes into the pinned
+  // metadata block, so descriptors, lane orders and data go to the GPU in ONE
+  // copy, and copy, kernel and digests stay on one stream (profiles/
+  // r01_small_call_latency.log).  Only for chunks the runtime classified
+  // itself: under QSMD5_FLAG_HOST a caller's stray device pointer must not
+  // reach a CPU memcpy.
+  uint64_t inline_bytes = 0;
+  bool inline_data = slices.size() == 1 && !(flags & QSMD5_FLAG_HOST) && groups[0].ncols == 1;
+  if (inline_data) {
+    for (uint64_t L : host_len) inline_bytes += stage_bytes(L);
+    inline_data = inline_bytes <= kInlineBytes;
+  }
+  if (!inline_data) inline_bytes = 0;
+  if (!slices.empty() && !inline_data)
     if (int rc = r.d_staging.reserve(nregions * region)) return rc;
 
-  // Descriptors (device pointers) for every chunk, upfront; segment
-  // descriptors and lane->chunk maps for the multi-column slices behind them.
+  // One metadata block: descriptors (device pointers) for every chunk, then
+  // segment descriptors of the multi-column slices; the lane->chunk maps; the
+  // inline data.
   const size_t meta_bytes = n * sizeof(qsmd5_chunk) + nseg * sizeof(qsmd5_chunk);
   const size_t order_words = n + nseg;
-  if (int rc = r.h_desc.reserve(meta_bytes + 16)) return rc;
-  if (int rc = r.h_order.reserve(order_words * sizeof(uint32_t) + 16)) return rc;
+  const size_t desc_span = (meta_bytes + 255) & ~size_t(255);
+  const size_t order_span = (order_words * sizeof(uint32_t) + 255) & ~size_t(255);
+  const size_t data_off = desc_span + order_span;
+  const size_t block_bytes = data_off + inline_bytes;
+  if (int rc = r.h_meta.reserve(block_bytes + 256)) return rc;
+  if (int rc = r.d_meta.reserve(block_bytes + 256)) return rc;
   if (int rc = r.h_dig.reserve(n * 16 + 16)) return rc;
-  if (int rc = r.d_desc.reserve(meta_bytes + 16)) return rc;
-  if (int rc = r.d_order.reserve(order_words * sizeof(uint32_t) + 16)) return rc;
   if (int rc = r.d_dig.reserve(n * 16 + 16)) return rc;
   if (nseg)
     if (int rc = r.d_state.reserve(n * 16 + 16)) return rc;
-  qsmd5_chunk* hd = static_cast<qsmd5_chunk*>(r.h_desc.p);
+  uint8_t* hm = static_cast<uint8_t*>(r.h_meta.p);
+  uint8_t* dm = static_cast<uint8_t*>(r.d_meta.p);
+  qsmd5_chunk* hd = reinterpret_cast<qsmd5_chunk*>(hm);
   qsmd5_chunk* hseg = hd + n;
-  uint32_t* ho = static_cast<uint32_t*>(r.h_order.p);
+  uint32_t* ho = reinterpret_cast<uint32_t*>(hm + desc_span);
   uint32_t* hso = ho + n;
   for (size_t i = 0; i < n; ++i) hd[i] = {len[i] ? chunks[i].ptr : nullptr, len[i]};
-  uint8_t* stage = static_cast<uint8_t*>(r.d_staging.p);
+  uint8_t* stage = inline_data ? dm + data_off : static_cast<uint8_t*>(r.d_staging.p);
   std::vector<uint8_t*> slice_base(slices.size());
   for (size_t si = 0; si < slices.size(); ++si) {
     const qsmd5::Slice& sl = slices[si];
@@ -507,6 +534,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       } else {
         hd[ci].ptr = base + off;
       }
+      if (inline_data) memcpy(hm + data_off + off, chunks[ci].ptr, len[ci]);
       off += stage_bytes(col_bytes(len[ci], sl.col));
     }
   }
@@ -524,13 +552,11 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     for (hipStream_t s : r.compute) (void)hipStreamSynchronize(s);
     return code;
   };
-  QS_HIP(hipMemcpyAsync(r.d_desc.p, hd, meta_bytes, hipMemcpyHostToDevice, s0));
-  QS_HIP(hipMemcpyAsync(r.d_order.p, ho, order_words * sizeof(uint32_t), hipMemcpyHostToDevice, s0));
-  hipEvent_t meta_ready = nullptr, k_first = nullptr, k_last = nullptr;
-  if (int rc = events.make(&meta_ready, hipEventDisableTiming)) return drain(rc);
-  if (int rc = events.make(&k_first, hipEventDefault)) return drain(rc);
-  if (int rc = events.make(&k_last, hipEventDefault)) return drain(rc);
-  QS_HIP(hipEventRecord(meta_ready, s0));
+  QS_HIP(hipMemcpyAsync(dm, hm, block_bytes, hipMemcpyHostToDevice, s0));
+  // A single slice runs entirely on s0 (copy, then kernel: stream order, no
+  // events); several slices overlap copies and kernels over the streams.
+  const bool one_stream = slices.size() <= 1;
+  if (!one_stream) QS_HIP(hipEventRecord(r.ev_meta, s0));
   std::vector<hipEvent_t> region_free(nregions, nullptr);
   // QSMD5_TRACE=1: per-slice copy/kernel timeline on stderr (diagnostics).
   const bool trace = env_u64("QSMD5_TRACE", 0) != 0;
@@ -538,20 +564,22 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   for (auto& ev : tr)
     if (int rc = events.make(&ev, hipEventDefault)) return drain(rc);
   if (trace) QS_HIP(hipEventRecord(tr.back(), s0));
-  const uint32_t* d_order = static_cast<const uint32_t*>(r.d_order.p);
-  const qsmd5_chunk* d_seg = static_cast<const qsmd5_chunk*>(r.d_desc.p) + n;
+  const uint32_t* d_order = reinterpret_cast<const uint32_t*>(dm + desc_span);
+  const qsmd5_chunk* d_desc = reinterpret_cast<const qsmd5_chunk*>(dm);
+  const qsmd5_chunk* d_seg = d_desc + n;
   uint32_t* d_dig = static_cast<uint32_t*>(r.d_dig.p);
   bool first_kernel = true;
+  unsigned used = 0;  // compute streams (1..) that ran work: joined into s0 at the end
   auto mark_first = [&](hipStream_t s) -> int {
     if (first_kernel) {
-      QS_HIP(hipEventRecord(k_first, s));
+      QS_HIP(hipEventRecord(r.ev_first, s));
       first_kernel = false;
     }
     return 0;
   };
   auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt, bool aligned16) -> int {
     if (int rc = mark_first(s)) return rc;
-    hipError_t e = qsmd5::launch_batch(r.d_desc.p, ord, (uint32_t)cnt, d_dig,
+    hipError_t e = qsmd5::launch_batch(d_desc, ord, (uint32_t)cnt, d_dig,
                                        kernel_choice(cnt, aligned16), s);
     if (e != hipSuccess) return hip_fail(e, "qsmd5 kernel launch");
     return 0;
@@ -573,8 +601,10 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     const qsmd5::Slice& sl = slices[si];
     const qsmd5::Group& g = groups[sl.group];
     const size_t reg = si % nregions;
-    hipStream_t cs = r.compute[1 + sl.group % (kComputeStreams - 1)];
-    hipStream_t cp = r.copy[si % r.ncopy];
+    const int csi = one_stream ? 0 : 1 + (int)(sl.group % (kComputeStreams - 1));
+    hipStream_t cs = r.compute[csi];
+    hipStream_t cp = one_stream ? s0 : r.copy[si % r.ncopy];
+    used |= 1u << csi;
     if (region_free[reg]) {
       hipError_t e = hipStreamWaitEvent(cp, region_free[reg], 0);
       if (e != hipSuccess) return drain(hip_fail(e, "hipStreamWaitEvent"));
@@ -582,7 +612,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     const uint64_t col_off = W == kNoColumns ? 0 : (uint64_t)sl.col * W;
     uint8_t* dst = slice_base[si];
     if (trace) QS_HIP(hipEventRecord(tr[4 * si], cp));
-    for (size_t k = 0; k < sl.active;) {
+    for (size_t k = 0; k < sl.active && !inline_data;) {
       const uint32_t ci = host_idx[g.first + k];
       const uint64_t w = col_bytes(len[ci], sl.col);
       const uint8_t* src = static_cast<const uint8_t*>(chunks[ci].ptr) + col_off;
@@ -624,14 +654,16 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       dst += rows * stage_bytes(w);
       k += rows;
     }
-    hipEvent_t copied = nullptr, done = nullptr;
-    if (int rc = events.make(&copied, hipEventDisableTiming)) return drain(rc);
-    if (int rc = events.make(&done, hipEventDisableTiming)) return drain(rc);
     if (trace) QS_HIP(hipEventRecord(tr[4 * si + 1], cp));
-    hipError_t e = hipEventRecord(copied, cp);
-    if (e == hipSuccess) e = hipStreamWaitEvent(cs, copied, 0);
-    if (e == hipSuccess) e = hipStreamWaitEvent(cs, meta_ready, 0);
-    if (e != hipSuccess) return drain(hip_fail(e, "stream ordering"));
+    hipError_t e = hipSuccess;
+    if (!one_stream) {
+      hipEvent_t copied = nullptr;
+      if (int rc = events.make(&copied, hipEventDisableTiming)) return drain(rc);
+      e = hipEventRecord(copied, cp);
+      if (e == hipSuccess) e = hipStreamWaitEvent(cs, copied, 0);
+      if (e == hipSuccess) e = hipStreamWaitEvent(cs, r.ev_meta, 0);
+      if (e != hipSuccess) return drain(hip_fail(e, "stream ordering"));
+    }
     if (trace) QS_HIP(hipEventRecord(tr[4 * si + 2], cs));
     if (g.ncols > 1) {
       if (int rc = mark_first(cs)) return drain(rc);
@@ -643,19 +675,24 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       if (int rc = launch(cs, d_order + dev_idx.size() + g.first, sl.active, true))
         return drain(rc);
     }
-    if ((e = hipEventRecord(done, cs)) != hipSuccess) return drain(hip_fail(e, "hipEventRecord"));
+    if (!one_stream && nregions < slices.size()) {  // a later slice reuses this region
+      hipEvent_t done = nullptr;
+      if (int rc = events.make(&done, hipEventDisableTiming)) return drain(rc);
+      if ((e = hipEventRecord(done, cs)) != hipSuccess) return drain(hip_fail(e, "hipEventRecord"));
+      region_free[reg] = done;
+    }
     if (trace) QS_HIP(hipEventRecord(tr[4 * si + 3], cs));
-    region_free[reg] = done;
   }
-  // Join every compute stream into s0, then fetch the digests.
+  // Join the compute streams that ran work into s0, then fetch the digests.
   for (int k = 1; k < kComputeStreams; ++k) {
+    if (!(used & (1u << k))) continue;
     hipEvent_t j = nullptr;
     if (int rc = events.make(&j, hipEventDisableTiming)) return drain(rc);
     hipError_t e = hipEventRecord(j, r.compute[k]);
     if (e == hipSuccess) e = hipStreamWaitEvent(s0, j, 0);
     if (e != hipSuccess) return drain(hip_fail(e, "stream join"));
   }
-  if (!first_kernel) QS_HIP(hipEventRecord(k_last, s0));
+  if (!first_kernel) QS_HIP(hipEventRecord(r.ev_last, s0));
   QS_HIP(hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0));
   hipError_t e = hipStreamSynchronize(s0);
   if (e != hipSuccess) return drain(hip_fail(e, "hipStreamSynchronize"));
@@ -679,7 +716,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   }
   float kms = 0;
   r.last_kernel_ms =
-      (!first_kernel && hipEventElapsedTime(&kms, k_first, k_last) == hipSuccess) ? kms : 0.0;
+      (!first_kernel && hipEventElapsedTime(&kms, r.ev_first, r.ev_last) == hipSuccess) ? kms : 0.0;
   r.last_wall_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return 0;
