@@ -1,0 +1,88 @@
+"""Randomised batches through qsmd5_hash_batch_ex, every digest against the oracle.
+
+Each seeded batch mixes lengths (0 B .. ~2 MiB, log-uniform, padding edges
+included), memory kinds (device, pinned host, pageable host), byte offsets,
+duplicates, and the runtime's knobs drawn per batch:
+- QSMD5_COLUMN_BYTES: automatic, whole chunks, or a forced width;
+- QSMD5_KERNEL: automatic or forced;
+- QSMD5_MAPS_AFTER: VMA classification on early or off;
+- QSMD5_FLAG_HOST: when every chunk is host memory.
+This drives the paths the fixed tests pin one at a time: the inline small-batch
+path, single- and multi-slice staging, column kernels, the classifier's range
+caches and 2-D copy runs.
+"""
+import ctypes
+import os
+import random
+
+import numpy as np
+import pytest
+
+import qsmd5
+from oracle_util import md5_many
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+POOL = 24 << 20
+EDGES = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 4095, 4096, 4097]
+
+
+@pytest.fixture(scope="module")
+def pools():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert qsmd5.lib().qsmd5_init(0) == 0
+    rng = np.random.default_rng(2024)
+    host = rng.integers(0, 256, size=POOL, dtype=np.uint8)
+    dev = torch.from_numpy(host.copy()).cuda()
+    pp = qsmd5.alloc_pinned(POOL)
+    pinned = np.ctypeslib.as_array((ctypes.c_uint8 * POOL).from_address(pp))
+    pinned[:] = host
+    torch.cuda.synchronize()
+    yield {"host": host, "dev": dev, "pinned": pinned}
+    qsmd5.free_pinned(pp)
+    for k in ("QSMD5_COLUMN_BYTES", "QSMD5_KERNEL", "QSMD5_MAPS_AFTER"):
+        os.environ.pop(k, None)
+
+
+def _length(rng):
+    if rng.random() < 0.2:
+        return rng.choice(EDGES)
+    return int(2 ** rng.uniform(0, 21)) + rng.randrange(97)
+
+
+@pytest.mark.parametrize("seed", range(64))
+def test_random_batches(pools, seed):
+    rng = random.Random(seed)
+    n = rng.choice([1, 2, 3, 17, 64, 65, 200, 300])
+    kinds = rng.choice([["dev"], ["pinned"], ["host"], ["pinned", "host"], ["dev", "pinned", "host"]])
+    chunks, refs = [], []
+    for _ in range(n):
+        L = _length(rng)
+        off = rng.randrange(POOL - L)
+        k = rng.choice(kinds)
+        if k == "dev":
+            ptr = pools["dev"].data_ptr() + off
+        else:
+            ptr = pools[k].ctypes.data + off
+        chunks.append((ptr if L else 0, L))
+        refs.append((pools["host"].ctypes.data + off, L))
+    if n > 2 and rng.random() < 0.3:  # duplicates
+        chunks += chunks[:2]
+        refs += refs[:2]
+    env = {
+        "QSMD5_COLUMN_BYTES": rng.choice([None, None, "0", "1024", "4160", str(256 << 10)]),
+        "QSMD5_KERNEL": rng.choice([None, None, "pc", "pc2", "v1", "coal"]),
+        "QSMD5_MAPS_AFTER": rng.choice([None, "1", "100000000"]),
+    }
+    for k, v in env.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
+    flags = qsmd5.FLAG_HOST if "dev" not in kinds and rng.random() < 0.5 else 0
+    got = qsmd5.hash_batch(chunks, flags=flags)
+    want = md5_many(refs)
+    assert got == want, (seed, n, kinds, env, flags,
+                         [i for i, (a, b) in enumerate(zip(got, want)) if a != b][:5])
