@@ -937,7 +937,7 @@ void run_group(Request* first) noexcept {
 int group_commit(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
   if (env_u64("QSMD5_NO_COALESCE", 0)) return run_any(chunks, n, digests, flags);
   Coalescer& co = coalescer();
-  Request req{chunks, n, digests, flags};
+  Request req{chunks, n, digests, flags, 0, std::string(), false, nullptr};
   // Linger: callers released by the previous launch usually re-submit within
   // microseconds (a worker loop hashing part after part).  A new leader waits
   // up to this long for as many requests as the previous group held, so they
