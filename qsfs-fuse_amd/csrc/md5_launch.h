@@ -38,6 +38,7 @@ hipError_t launch_column(const void* segs, const uint32_t* order, uint32_t n, ui
 hipError_t launch_blocks(uint32_t* state, const uint8_t* p, uint32_t nblk, hipStream_t s);
 hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint64_t total_len,
                         hipStream_t s);
+hipError_t warm_up(hipStream_t s);
 hipError_t launch_lcg_fill(uint8_t* base, uint64_t stride, uint64_t len, uint32_t seed0,
                            uint32_t nchunks, hipStream_t s);
 

@@ -223,6 +223,9 @@ int init_dev(Dev& d, int device) {
       (e = hipEventCreateWithFlags(&d.ev_first, hipEventDefault)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&d.ev_last, hipEventDefault)) != hipSuccess)
     return hip_fail(e, "hipEventCreate");
+  if ((e = qsmd5::warm_up(d.compute[0])) != hipSuccess ||
+      (e = hipStreamSynchronize(d.compute[0])) != hipSuccess)
+    return hip_fail(e, "qsmd5: kernel warm-up (is this a gfx950 GPU?)");
   return 0;
 }
 
