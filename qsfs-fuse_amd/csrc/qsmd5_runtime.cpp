@@ -1012,8 +1012,10 @@ int guarded(F&& f) {
 struct qsmd5_ctx {
   uint32_t* d_state = nullptr;  // 4 words
   uint8_t* d_tail = nullptr;    // 64 bytes
+  uint8_t* d_seg = nullptr;     // 64 bytes: column segment descriptor, lane order {0}, spare
   uint8_t* d_stage = nullptr;   // staging for host updates
   size_t stage_cap = 0;
+  uint64_t hashed = 0;          // bytes folded into d_state (whole blocks)
   uint8_t tail[64];
   uint32_t tail_len = 0;
   uint64_t total = 0;
@@ -1263,6 +1265,8 @@ int qsmd5_ctx_create(qsmd5_ctx** out) {
     const uint32_t init[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
     hipError_t e = hipMalloc(&c->d_state, 16);
     if (e == hipSuccess) e = hipMalloc(&c->d_tail, 64);
+    if (e == hipSuccess) e = hipMalloc(&c->d_seg, 64);
+    if (e == hipSuccess) e = hipMemset(c->d_seg, 0, 64);  // lane order word = chunk 0
     if (e == hipSuccess) e = hipMemcpy(c->d_state, init, 16, hipMemcpyHostToDevice);
     if (e != hipSuccess) {
       qsmd5_ctx_destroy(c);
@@ -1277,6 +1281,7 @@ void qsmd5_ctx_destroy(qsmd5_ctx* c) {
   if (!c) return;
   if (c->d_state) (void)hipFree(c->d_state);
   if (c->d_tail) (void)hipFree(c->d_tail);
+  if (c->d_seg) (void)hipFree(c->d_seg);
   if (c->d_stage) (void)hipFree(c->d_stage);
   delete c;
 }
@@ -1297,13 +1302,24 @@ static int ctx_blocks(qsmd5_ctx* c, const uint8_t* p, uint64_t nblk, bool on_dev
     QS_HIP(hipMemcpyAsync(c->d_stage, p, bytes, hipMemcpyHostToDevice, s));
     src = c->d_stage;
   }
+  // The blocks run as one column of a one-lane column batch: the latency
+  // kernel's producer/consumer chain (~1207 cycles/block) instead of a lone
+  // lane doing its own loads (64 MiB in 1 MiB updates: 1.0 s -> see
+  // profiles/r01_stream_ctx_rate.log).  The segment's total length is set one
+  // block past the update, so the chain always parks its state in d_state and
+  // never finalises; qsmd5_ctx_final runs the tail.
   while (nblk) {
-    const uint32_t step = (uint32_t)std::min<uint64_t>(nblk, 0x40000000ull);
-    QS_HIP(qsmd5::launch_blocks(c->d_state, src, step, s));
-    src += (uint64_t)step * 64;
+    const uint64_t step = std::min<uint64_t>(nblk, 0x40000000ull);
+    const qsmd5_chunk seg = {src, c->hashed + step * 64 + 64};
+    QS_HIP(hipMemcpyAsync(c->d_seg, &seg, sizeof(seg), hipMemcpyHostToDevice, s));
+    QS_HIP(qsmd5::launch_column(c->d_seg, reinterpret_cast<const uint32_t*>(c->d_seg + 16), 1,
+                                reinterpret_cast<uint32_t*>(c->d_seg + 32), c->hashed, step * 64,
+                                c->d_state, s));
+    QS_HIP(hipStreamSynchronize(s));  // seg lives on this stack frame
+    src += step * 64;
+    c->hashed += step * 64;
     nblk -= step;
   }
-  QS_HIP(hipStreamSynchronize(s));
   return 0;
 }
 
