@@ -16,8 +16,8 @@
 //   qsmd5_column_pc[2]_kernel  the latency kernels over one column of a
 //                            host-staged batch: chains resume from and park in
 //                            HBM state (qsmd5_runtime.cpp run_batch).
-// Streaming kernels (the MD5 class, MD5.cpp:240-312):
-//   qsmd5_blocks_kernel      advances one state over whole blocks (update()).
+// Streaming (the MD5 class, MD5.cpp:240-312): update() runs its blocks as a
+// one-lane qsmd5_column_pc_kernel batch; then
 //   qsmd5_final_kernel       tail + padding + length (finalize()).
 // Test/bench support:
 //   qsmd5_lcg_fill_kernel    SURVEY.md §8c LCG data, jump-ahead parallel.
@@ -287,22 +287,6 @@ extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_kernel(
   hash_message(st, cd.ptr, cd.len);
   u32x4 o = {st[0], st[1], st[2], st[3]};
   *reinterpret_cast<u32x4*>(digests + 4u * (uint64_t)idx) = o;
-}
-
-// Streaming update: state[4] advanced over nblk whole blocks at p.
-extern "C" __global__ __launch_bounds__(64) void qsmd5_blocks_kernel(uint32_t* __restrict__ state,
-                                                                     const uint8_t* p,
-                                                                     uint32_t nblk) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint32_t st[4] = {state[0], state[1], state[2], state[3]};
-  if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0)
-    blocks_aligned4(st, reinterpret_cast<const uint32_t*>(p), nblk);
-  else
-    blocks_unaligned(st, p, nblk);
-  state[0] = st[0];
-  state[1] = st[1];
-  state[2] = st[2];
-  state[3] = st[3];
 }
 
 // Streaming finalize: tail bytes (< 64, host-provided in device memory) + pad.
@@ -779,11 +763,6 @@ hipError_t launch_column(const void* segs, const uint32_t* order, uint32_t n, ui
   return hipGetLastError();
 }
 
-hipError_t launch_blocks(uint32_t* state, const uint8_t* p, uint32_t nblk, hipStream_t s) {
-  if (nblk == 0) return hipSuccess;
-  hipLaunchKernelGGL(qsmd5_blocks_kernel, dim3(1), dim3(64), 0, s, state, p, nblk);
-  return hipGetLastError();
-}
 
 hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint64_t total_len,
                         hipStream_t s) {

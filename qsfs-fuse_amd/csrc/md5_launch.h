@@ -35,7 +35,6 @@ hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, u
 // digest lands in digests[4 * order[t]] after the chunk's last column.
 hipError_t launch_column(const void* segs, const uint32_t* order, uint32_t n, uint32_t* digests,
                          uint64_t col_off, uint64_t col_w, uint32_t* states, hipStream_t s);
-hipError_t launch_blocks(uint32_t* state, const uint8_t* p, uint32_t nblk, hipStream_t s);
 hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint64_t total_len,
                         hipStream_t s);
 hipError_t warm_up(hipStream_t s);
