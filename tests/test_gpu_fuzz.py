@@ -86,3 +86,24 @@ def test_random_batches(pools, seed):
     want = md5_many(refs)
     assert got == want, (seed, n, kinds, env, flags,
                          [i for i, (a, b) in enumerate(zip(got, want)) if a != b][:5])
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_stream_updates(pools, seed):
+    """The MD5 class (qsmd5_ctx): random pieces from host and device memory, so
+    the host-side tail and the one-lane column launches meet every split."""
+    rng = random.Random(1000 + seed)
+    start = rng.randrange(4096)
+    pos, pieces = start, []
+    for _ in range(rng.randrange(1, 40)):
+        L = rng.choice([0, 1, 63, 64, 65, 127, rng.randrange(1, 5000), rng.randrange(1, 300000)])
+        if pos + L > POOL:
+            break
+        pieces.append((pos, L, rng.choice(["host", "pinned", "dev"])))
+        pos += L
+    h = qsmd5.MD5()
+    for off, L, k in pieces:
+        base = pools["dev"].data_ptr() if k == "dev" else pools[k].ctypes.data
+        h.update((base + off if L else 0, L))
+    want = md5_many([(pools["host"].ctypes.data + start, pos - start)])[0]
+    assert h.finalize().digest() == want, (seed, [(L, k) for _, L, k in pieces])
