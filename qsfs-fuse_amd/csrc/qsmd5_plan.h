@@ -15,10 +15,10 @@
 // does.  W = kNoColumns (chunks no longer than a column) degenerates to
 // whole-chunk row slices.
 //
-// Staged segments are packed at 256-B alignment plus a 4 KiB + 256 B skew, so
-// that equal-size parts never sit at a power-of-two stride (the lanes of a
-// wave walk their chunks in lockstep; a power-of-two stride sends every lane's
-// request to the same HBM channel).
+// Staged segments are packed at 256-B alignment, segments of 16 KiB and more
+// plus a 4 KiB + 256 B skew, so that equal-size parts never sit at a
+// power-of-two stride (the lanes of a wave walk their chunks in lockstep; a
+// power-of-two stride sends every lane's request to the same HBM channel).
 #pragma once
 
 #include <stdint.h>
@@ -38,8 +38,17 @@ constexpr uint64_t kColMin = 256ull << 10;   // ... and at least this: 2-D copie
 constexpr uint64_t kColMaxPerChunk = 1024;   // automatic columns per chunk (launches per group)
 constexpr uint64_t kNoColumns = ~0ull;
 
-// Bytes one staged segment of L message bytes occupies in a region.
-inline uint64_t stage_bytes(uint64_t L) { return ((L + kAlign - 1) & ~(kAlign - 1)) + kSkew; }
+constexpr uint64_t kSkewFrom = 16ull << 10;  // segments this long or longer get the skew
+
+// Bytes one staged segment of L message bytes occupies in a region.  The skew
+// is for long equal segments, whose lanes walk in lockstep at a power-of-two
+// stride; short ones (a wave's 64 lanes inside 1 MiB) spread over the channels
+// anyway (1 M x 1 KiB device-resident at an exact stride: 58.6% of HBM peak,
+// profiles/r01_saturation_tiny.jsonl), and skewing them would stage 1 KiB
+// objects at 5.25 KiB each.
+inline uint64_t stage_bytes(uint64_t L) {
+  return ((L + kAlign - 1) & ~(kAlign - 1)) + (L >= kSkewFrom ? kSkew : 0);
+}
 
 struct Group {
   size_t first, count;  // range in the host lane order
