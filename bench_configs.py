@@ -9,7 +9,16 @@
   5  10 000 x 10 MiB (97.7 GiB) on ONE GPU, device-resident (the per-GPU share at
      N GPUs is 10000/N; the 8-GPU run is the driver's bench.py --gpus 8)
   sat  kernel-quality line: enough independent chains to need the HBM roofline
-     (131072 x 64 KiB, one-wave kernel)
+     (131072 x 64 KiB and x 256 KiB, coalesced kernel)
+Further lines, on request:
+  3p / 3cmp / 3cols  config 3 from pageable memory; pinned vs pageable at equal
+     sizes; 64 / 1024 / 4096 parts (column-width sweeps via QSMD5_COLUMN_BYTES)
+  5h   config 5 host-resident (10000 x 10 MiB from pinned memory)
+  small  1 M x 1 KiB objects from pageable (with and without QSMD5_FLAG_HOST)
+     and pinned memory
+  pool   512 pool buffers passed in pool order and shuffled
+  tiny   device-resident 1 M x 1 KiB, 1 M x 4 KiB, 512 K x 16 KiB
+  satpad saturation at exact power-of-two strides vs padded
 
 Every digest is checked against the reference-produced golden fixtures where
 they exist.  One JSON object per config on stdout.
