@@ -912,7 +912,11 @@ void run_group(Request* first) noexcept {
   int rc = 0;
   try {
     size_t total = 0;
-    for (Request* q = first; q; q = q->next) total += q->n;
+    int all_host = QSMD5_FLAG_HOST;  // kept only if every merged caller vouches for its chunks
+    for (Request* q = first; q; q = q->next) {
+      total += q->n;
+      all_host &= q->flags;
+    }
     std::vector<qsmd5_chunk> merged;
     merged.reserve(total);
     for (Request* q = first; q; q = q->next)
@@ -922,7 +926,7 @@ void run_group(Request* first) noexcept {
         merged.push_back(c);
       }
     std::vector<uint8_t> dig(16 * total);
-    rc = run_any(merged.data(), total, reinterpret_cast<uint8_t(*)[16]>(dig.data()), 0);
+    rc = run_any(merged.data(), total, reinterpret_cast<uint8_t(*)[16]>(dig.data()), all_host);
     if (rc == 0) {
       size_t off = 0;
       for (Request* q = first; q; q = q->next) {

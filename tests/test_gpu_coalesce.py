@@ -90,6 +90,30 @@ def test_truncate_flag_stays_per_caller():
         assert kind == "ok" and val == [want]
 
 
+def test_host_flag_stays_per_caller():
+    """QSMD5_FLAG_HOST is a caller's promise about its own chunks: a merged
+    batch keeps it only if every merged caller made it, so callers passing
+    device buffers without the flag still hash correctly beside flagged ones."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    L = 2 * MiB
+    bufs = [lcg_bytes(900 + i, L) for i in range(6)]
+    want = md5_many([(b, L) for b in bufs])
+    devs = [torch.frombuffer(bytearray(bytes(b)), dtype=torch.uint8).cuda() for b in bufs]
+    torch.cuda.synchronize()
+    fns = []
+    for i in range(6):
+        if i % 2:
+            fns.append(lambda i=i: qsmd5.hash_batch([(devs[i].data_ptr(), L)]))
+        else:
+            fns.append(lambda i=i: qsmd5.hash_batch([(ctypes.addressof(bufs[i]), L)],
+                                                    flags=qsmd5.FLAG_HOST))
+    for rnd in range(3):
+        for i, (kind, val) in enumerate(_threads(fns)):
+            assert kind == "ok" and val == [want[i]], (rnd, i, kind, val)
+
+
 TIMING_SCRIPT = r'''
 import ctypes, json, sys, threading, time
 import qsmd5
