@@ -4,8 +4,9 @@
 // This is the batch caller of SURVEY.md §8f row 1 in tool form:
 //   1. slice each file into upload parts exactly like
 //      QSTransferManager::PrepareUpload (QSTransferManager.cpp:475-550);
-//   2. gather every part into pinned host memory -- the ResourceManager pool
-//      (ResourceManager.cpp:53-77) made of qsmd5_alloc_pinned buffers;
+//   2. map each file (mmap, read-only): the batch's H2D copies read the page
+//      cache directly, with no read() copy and no pinned buffer (pageable host
+//      memory hashes as fast as pinned: DESIGN.md §5);
 //   3. hash all parts of all files in ONE qsmd5_hash_batch call instead of one
 //      md5(buffer) per part (QSClient.cpp:370, 446).
 //
@@ -14,9 +15,13 @@
 //   and one line per part for larger files (or for every file with --parts):
 //   "<md5>  <file>#<part> <offset> <size>"
 // Exit status: 0 ok, 1 usage or I/O error, 2 GPU error.
+#include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <string>
 #include <vector>
@@ -29,37 +34,35 @@ struct FileParts {
   std::string path;
   uint64_t size = 0;
   std::vector<qsmd5_part> parts;
-  uint8_t* data = nullptr;  // pinned
+  const uint8_t* data = nullptr;  // the file, mapped read-only (nullptr when empty)
 };
 
 bool read_file(const char* path, FileParts& f, std::string& err) {
-  FILE* fp = fopen(path, "rb");
-  if (!fp) {
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) {
     err = std::string("cannot open ") + path;
     return false;
   }
-  if (fseeko(fp, 0, SEEK_END) != 0) {
-    fclose(fp);
-    err = std::string("cannot seek ") + path;
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    err = std::string("cannot stat ") + path;
     return false;
   }
-  const off_t sz = ftello(fp);
-  fseeko(fp, 0, SEEK_SET);
   f.path = path;
-  f.size = (uint64_t)sz;
-  void* p = nullptr;
-  if (qsmd5_alloc_pinned(f.size ? f.size : 1, &p) != 0) {
-    fclose(fp);
-    err = std::string("pinned allocation failed: ") + qsmd5_last_error();
-    return false;
+  f.size = (uint64_t)st.st_size;
+  if (f.size) {
+    void* p = mmap(nullptr, f.size, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (p == MAP_FAILED) {
+      close(fd);
+      err = std::string("cannot map ") + path;
+      return false;
+    }
+    (void)madvise(p, f.size, MADV_SEQUENTIAL);
+    (void)madvise(p, f.size, MADV_WILLNEED);  // start readahead of the whole file
+    f.data = static_cast<const uint8_t*>(p);
   }
-  f.data = static_cast<uint8_t*>(p);
-  size_t got = f.size ? fread(f.data, 1, f.size, fp) : 0;
-  fclose(fp);
-  if (got != f.size) {
-    err = std::string("short read ") + path;
-    return false;
-  }
+  close(fd);  // the mapping stays valid
   return true;
 }
 
@@ -140,6 +143,6 @@ int main(int argc, char** argv) {
     }
   }
   for (FileParts& f : fs)
-    if (f.data) qsmd5_free_pinned(f.data);
+    if (f.data) munmap(const_cast<uint8_t*>(f.data), f.size);
   return rc;
 }
