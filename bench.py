@@ -113,22 +113,21 @@ def _cpu_model():
 
 
 def _traffic_from_profiles():
-    """HBM bytes per launch from the committed PMC summary (profiles/*traffic*.json)."""
+    """HBM bytes per launch of the headline kernel from the newest committed PMC
+    summary for this workload (profiles/<round>_*traffic.json)."""
     pdir = os.path.join(ROOT, "profiles")
-    best = None
+    found = None
     if os.path.isdir(pdir):
-        for f in sorted(os.listdir(pdir)):
-            if f.endswith("_traffic.json"):
-                best = os.path.join(pdir, f)
-    if not best:
-        return None
-    try:
-        d = json.load(open(best))
-        if d.get("workload") == "batch512x10MiB":
-            return d.get("hbm_read_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
-    return None
+        for f in sorted(os.listdir(pdir)):  # round-prefixed names: the last match is the newest
+            if not f.endswith("traffic.json"):
+                continue
+            try:
+                d = json.load(open(os.path.join(pdir, f)))
+            except (OSError, ValueError):
+                continue
+            if isinstance(d, dict) and d.get("workload") == "batch512x10MiB":
+                found = d.get("hbm_read_bytes_per_launch")
+    return found
 
 
 def main():
