@@ -36,6 +36,7 @@
 #include "../../include/qsmd5.h"
 #include "md5_launch.h"
 #include "qsmd5_plan.h"
+#include "qsmd5_vma.h"
 
 namespace {
 
@@ -359,28 +360,16 @@ class Classifier {
     next_ = (next_ + 1) % kRanges;
     used_ = used_ < kRanges ? used_ + 1 : kRanges;
   }
-  // Readable VMAs that are anonymous, [heap]/[stack]/[anon:...], or regular
-  // files outside /dev; anything else (device files, dma-bufs, anon inodes)
-  // is left to the per-pointer query.
+  // The VMAs qsmd5_vma.h lets us cache as host memory; anything else (device
+  // files, dma-bufs, anon inodes) is left to the per-pointer query.
   void read_maps() {
     maps_read_ = true;
     FILE* f = fopen("/proc/self/maps", "r");
     if (!f) return;
     char line[4096];
-    while (fgets(line, sizeof(line), f)) {
-      unsigned long long lo = 0, hi = 0;
-      char perms[8] = {0};
-      int path_at = 0;
-      if (sscanf(line, "%llx-%llx %7s %*s %*s %*s %n", &lo, &hi, perms, &path_at) < 3) continue;
-      if (perms[0] != 'r' || hi <= lo) continue;
-      const char* path = line + path_at;
-      while (*path == ' ') ++path;
-      const bool anon = *path == '\n' || *path == 0;
-      const bool special = *path == '[' && (!strncmp(path, "[heap]", 6) || !strncmp(path, "[stack]", 7) ||
-                                           !strncmp(path, "[anon:", 6));
-      const bool file = *path == '/' && strncmp(path, "/dev/", 5) != 0;
-      if (anon || special || file) vmas_.push_back(Vma{(uintptr_t)lo, (uintptr_t)hi});
-    }
+    uint64_t lo = 0, hi = 0;
+    while (fgets(line, sizeof(line), f))
+      if (qsmd5::host_vma_from_maps_line(line, &lo, &hi)) vmas_.push_back(Vma{(uintptr_t)lo, (uintptr_t)hi});
     fclose(f);
   }
   struct Range {
