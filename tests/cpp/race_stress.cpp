@@ -1,0 +1,178 @@
+// tests/cpp/race_stress.cpp -- concurrent callers of every C-ABI entry point
+// qsfs reaches from several threads at once, for the host-sanitizer builds
+// (scripts/build_sanitized.sh: the runtime's host code under ThreadSanitizer,
+// and under AddressSanitizer + UBSan).
+//
+// The reference calls md5() from FUSE threads and from up to `numtransfer`
+// executor workers at the same time (TransferManager.cpp:55-60,
+// QSClient.cpp:370, 446) and has no race detection of its own.
+// The C-ABI promises to be reentrant, so T threads here race:
+//   - qsmd5_init (lazy, call_once) as their first call;
+//   - qsmd5_hash_one over pageable buffers (group commit merges these);
+//   - qsmd5_hash_batch / _ex over ragged, unaligned sub-ranges;
+//   - the streaming context (MD5 class) fed in pieces;
+//   - qsmd5_alloc_pinned / qsmd5_free_pinned around a hash;
+//   - qsmd5_hex / qsmd5_base64.
+// Every digest is checked against the CPU oracle (oracle/md5_oracle.c, the
+// checker, linked only into this test).
+// usage: race_stress [threads=6] [rounds=12] [max_len=3145728] [racy]
+// `racy` adds a deliberate unsynchronised counter shared by the threads: the
+// negative control showing that the TSan build, with its HIP suppressions,
+// still reports a race in instrumented code.
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <atomic>
+#include <thread>
+#include <vector>
+
+#include "../../include/qsmd5.h"
+
+extern "C" void oracle_md5(const uint8_t* p, uint64_t len, uint8_t out[16]);
+extern "C" void oracle_lcg_fill(uint8_t* dst, uint64_t len, uint32_t seed);
+
+namespace {
+
+std::atomic<int> g_bad{0};
+std::atomic<long> g_checked{0};
+bool g_racy = false;
+long g_racy_counter = 0;  // written without a lock when g_racy (negative control)
+
+void check(const uint8_t* p, uint64_t len, const uint8_t got[16], const char* what, int t, int r) {
+  uint8_t want[16];
+  oracle_md5(p, len, want);
+  g_checked.fetch_add(1);
+  if (memcmp(want, got, 16) != 0) {
+    char a[33], b[33];
+    qsmd5_hex(got, a);
+    qsmd5_hex(want, b);
+    fprintf(stderr, "MISMATCH %s thread %d round %d len %llu: %s != %s\n", what, t, r,
+            (unsigned long long)len, a, b);
+    g_bad.fetch_add(1);
+  }
+}
+
+void fail(const char* what, int rc, int t, int r) {
+  fprintf(stderr, "ERROR %s thread %d round %d: rc %d (%s) %s\n", what, t, r, rc, qsmd5_strerror(rc),
+          qsmd5_last_error());
+  g_bad.fetch_add(1);
+}
+
+// xorshift: per-thread, deterministic
+uint32_t next(uint32_t& s) {
+  s ^= s << 13;
+  s ^= s >> 17;
+  s ^= s << 5;
+  return s;
+}
+
+void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthreads) {
+  std::vector<uint8_t> buf(max_len + 64);
+  oracle_lcg_fill(buf.data(), buf.size(), 1000u + (uint32_t)t);
+  uint32_t s = 0x9e3779b9u * (uint32_t)(t + 1);
+  ready->fetch_add(1);
+  while (ready->load() < nthreads) {
+  }
+  int rc = qsmd5_init(0);
+  if (rc != 0) {
+    fail("init", rc, t, -1);
+    return;
+  }
+  for (int r = 0; r < rounds; ++r) {
+    uint8_t d[16];
+    switch ((t + r) % 4) {
+      case 0: {  // one part, pageable, arbitrary offset and length
+        const size_t off = next(s) % 61, len = next(s) % (max_len - 64) + 1;
+        if ((rc = qsmd5_hash_one(buf.data() + off, len, d)) != 0) fail("hash_one", rc, t, r);
+        else check(buf.data() + off, len, d, "hash_one", t, r);
+        break;
+      }
+      case 1: {  // ragged batch of sub-ranges, including an empty chunk
+        const int n = 1 + (int)(next(s) % 9);
+        std::vector<qsmd5_chunk> ch(n);
+        std::vector<uint8_t> dg(16 * n);
+        for (int i = 0; i < n; ++i) {
+          const size_t off = next(s) % 4099;
+          size_t len = i == 0 ? 0 : next(s) % (max_len / 4);
+          if (off + len > buf.size()) len = buf.size() - off;
+          ch[i].ptr = buf.data() + off;
+          ch[i].len = len;
+        }
+        rc = (r & 4) ? qsmd5_hash_batch_ex(ch.data(), n, (uint8_t(*)[16])dg.data(), QSMD5_FLAG_HOST)
+                     : qsmd5_hash_batch(ch.data(), n, (uint8_t(*)[16])dg.data());
+        if (rc != 0) fail("hash_batch", rc, t, r);
+        else
+          for (int i = 0; i < n; ++i)
+            check((const uint8_t*)ch[i].ptr, ch[i].len, dg.data() + 16 * i, "hash_batch", t, r);
+        break;
+      }
+      case 2: {  // streaming context (MD5 class: update()* then finalize())
+        qsmd5_ctx* c = nullptr;
+        if ((rc = qsmd5_ctx_create(&c)) != 0) {
+          fail("ctx_create", rc, t, r);
+          break;
+        }
+        const size_t len = next(s) % (max_len / 2) + 1;
+        size_t at = 0;
+        while (at < len && rc == 0) {
+          size_t piece = next(s) % (len / 3 + 70) + 1;
+          if (piece > len - at) piece = len - at;
+          rc = qsmd5_ctx_update(c, buf.data() + at, piece);
+          at += piece;
+        }
+        if (rc == 0) rc = qsmd5_ctx_final(c, d);
+        qsmd5_ctx_destroy(c);
+        if (rc != 0) fail("ctx", rc, t, r);
+        else check(buf.data(), len, d, "ctx", t, r);
+        break;
+      }
+      case 3: {  // pinned buffer from the pool API
+        const size_t len = next(s) % (max_len / 2) + 1;
+        void* p = nullptr;
+        if ((rc = qsmd5_alloc_pinned(len, &p)) != 0) {
+          fail("alloc_pinned", rc, t, r);
+          break;
+        }
+        memcpy(p, buf.data() + 7, len);
+        if ((rc = qsmd5_hash_one(p, len, d)) != 0) fail("hash_one(pinned)", rc, t, r);
+        else check((const uint8_t*)p, len, d, "hash_one(pinned)", t, r);
+        if ((rc = qsmd5_free_pinned(p)) != 0) fail("free_pinned", rc, t, r);
+        break;
+      }
+    }
+    if (g_racy) g_racy_counter += 1;
+    char hex[33], b64[25];
+    qsmd5_hex(d, hex);
+    qsmd5_base64(d, b64);
+    if (strlen(hex) != 32 || strlen(b64) != 24) {
+      fprintf(stderr, "bad hex/base64 length\n");
+      g_bad.fetch_add(1);
+    }
+  }
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  const int T = argc > 1 ? atoi(argv[1]) : 6;
+  const int R = argc > 2 ? atoi(argv[2]) : 12;
+  const size_t L = argc > 3 ? strtoull(argv[3], nullptr, 10) : (3u << 20);
+  if (T < 1 || R < 1 || L < 1024) {
+    fprintf(stderr, "usage: race_stress [threads>=1] [rounds>=1] [max_len>=1024]\n");
+    return 2;
+  }
+  g_racy = argc > 4 && strcmp(argv[4], "racy") == 0;
+  if (qsmd5_device_count() < 1) {
+    fprintf(stderr, "no GPU\n");
+    return 2;
+  }
+  std::atomic<int> ready{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) th.emplace_back(worker, t, R, L, &ready, T);
+  for (auto& x : th) x.join();
+  printf("race_stress %s: %d threads x %d rounds, %ld digests checked, %d failures\n",
+         g_bad.load() ? "FAILED" : "ok", T, R, g_checked.load(), g_bad.load());
+  return g_bad.load() ? 1 : 0;
+}
