@@ -553,6 +553,12 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_column_pc2_kernel(
 // The hardware adds that offset to the LDS destination as well as to the
 // global address, so the LDS base passed in (M0) is lowered by the same amount
 // (the caller pads the LDS buffer in front to keep it non-negative).
+// Cache policy (aux) of the coalesced kernel's LDS-DMA loads: 2 = nt (non-temporal).
+// Every byte is read once; nt ran the saturation lines 1-2 points of HBM peak
+// higher than the default policy, A/B/A/B on one box.
+#ifndef QS_COAL_AUX
+#define QS_COAL_AUX 2
+#endif
 template <int U, int kU, int kTB, int kS, int kCPI, bool kImm>
 __device__ __forceinline__ void coal_fast_group(uint32_t (&st)[4], const uint8_t* (&gp)[kS],
                                                 u32x4 (*tile_buf)[64][kS], uint32_t lane,
@@ -565,10 +571,10 @@ __device__ __forceinline__ void coal_fast_group(uint32_t (&st)[4], const uint8_t
         __builtin_amdgcn_global_load_lds(
             QS_GP(gp[i]),
             QS_LP(reinterpret_cast<uintptr_t>(&tile_buf[(U + 1) & 1][i * kCPI][0]) - kOff), 16,
-            kOff, 0);
+            kOff, QS_COAL_AUX);
       } else {
         __builtin_amdgcn_global_load_lds(QS_GP(gp[i]), QS_LP(&tile_buf[(U + 1) & 1][i * kCPI][0]),
-                                         16, 0, 0);
+                                         16, 0, QS_COAL_AUX);
         gp[i] += kTB * 64;
       }
     }
@@ -641,7 +647,8 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
       const uint32_t blk = min(tl * (uint32_t)kTB + (piece[i] >> 2), src_nblk[i] - 1u);
       const uint8_t* g = src_nblk[i] ? src[i] + (uint64_t)blk * 64u + (piece[i] & 3u) * 16u
                                      : dummy;
-      __builtin_amdgcn_global_load_lds(QS_GP(g), QS_LP(&tile_buf[b][i * kCPI][0]), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(QS_GP(g), QS_LP(&tile_buf[b][i * kCPI][0]), 16, 0,
+                                       QS_COAL_AUX);
     }
   };
   const uint32_t rswz = swz(lane);
