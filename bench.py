@@ -39,8 +39,45 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(host_chunks, gpu_hex, threads):
-    """Time the reference md5() (or the oracle port) on this host over the chunks."""
+def _host_topology():
+    """CPU model, sockets, physical cores, logical CPUs, affinity and cgroup quota."""
+    model, phys, sockets = "unknown", set(), set()
+    try:
+        pid = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model == "unknown":
+                model = v
+            elif k == "physical id":
+                pid = v
+                sockets.add(v)
+            elif k == "core id":
+                phys.add((pid, v))
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        quota = None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"cpu_model": model, "sockets": len(sockets) or None,
+            "physical_cores": len(phys) or None, "logical_cpus": os.cpu_count() or 0,
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota}
+
+
+def cpu_baseline(host_chunks, gpu_hex, gpu_value):
+    """Time the reference md5() (or the oracle port) on this host's cores over
+    the chunks: 1 thread (as deployed: one file's parts hashed serially,
+    File.cpp:639-644), 5 (qsfs numtransfer default), 16 (this box's CPU share)
+    and every logical CPU the host shows.  Both reference call forms are timed:
+    md5(std::string) (MD5.cpp:335-339) and the call site's md5(iostream)
+    (MD5.cpp:341-349, two extra copies)."""
     n = len(host_chunks)
     ptrs = (ctypes.c_void_p * n)(*host_chunks)
     lens = (ctypes.c_uint64 * n)(*([CHUNK] * n))
@@ -52,22 +89,22 @@ def cpu_baseline(host_chunks, gpu_hex, threads):
         R.ref_md5_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         R.ref_md5_release.argtypes = [ctypes.c_void_p]
 
-        def run(k, thr):
+        def run(k, thr, iostream=0):
             h = R.ref_md5_prepare(ptrs, lens, k)
             out = (ctypes.c_char * (33 * k))()
             t0 = time.perf_counter()
-            R.ref_md5_run(h, out, thr, 0)
+            R.ref_md5_run(h, out, thr, iostream)
             dt = time.perf_counter() - t0
             R.ref_md5_release(h)
             raw = bytes(out)
             return dt, [raw[33 * i:33 * i + 32].decode() for i in range(k)]
-        kind, what = "reference", "reference md5(std::string) (src/base/MD5.cpp:335-339, -O2)"
+        kind, what = "reference", "reference md5() from src/base/MD5.cpp (-O2)"
     else:
         O = ctypes.CDLL(os.path.join(ROOT, "oracle", "libmd5_oracle.so"))
         O.oracle_md5_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                        ctypes.c_void_p, ctypes.c_int]
 
-        def run(k, thr):
+        def run(k, thr, iostream=0):
             out = (ctypes.c_uint8 * (16 * k))()
             t0 = time.perf_counter()
             O.oracle_md5_batch(ptrs, lens, k, out, thr)
@@ -75,41 +112,50 @@ def cpu_baseline(host_chunks, gpu_hex, threads):
             raw = bytes(out)
             return dt, [raw[16 * i:16 * i + 16].hex() for i in range(k)]
         kind, what = "port", "oracle/md5_oracle.c (-O3)"
-    # all chunks on `threads` threads, twice (~13 core-s in all on 16); the mean
-    passes = [run(n, threads) for _ in range(2)]
-    dt = sum(p[0] for p in passes) / len(passes)
-    ref_hex = passes[0][1]
-    # as deployed: parts of a file hashed serially (1 thread, 16 chunks) and by
-    # qsfs's numtransfer = 5 upload workers (5 threads, 40 chunks)
-    dt1, _ = run(16, 1)
-    dt5, _ = run(40, 5)
-    gib = n * CHUNK / float(1 << 30)
+    topo = _host_topology()
+    nproc = min(256, topo["logical_cpus"] or 1)
+    gib = lambda k: k * CHUNK / float(1 << 30)
+    by_threads, by_threads_iostream, samples = {}, {}, {}
+    ref_hex = None
+    for thr, k in ((1, 16), (5, 40), (16, 128), (nproc, n)):
+        k = min(k, n)
+        run(min(thr, k), thr)  # wake the cores first (idle CPUs start slow)
+        passes = [run(k, thr) for _ in range(2)]
+        dt = min(p[0] for p in passes)  # best of 2: thread start-up skew, not hashing
+        by_threads[str(thr)] = round(gib(k) / dt, 3)
+        samples[str(thr)] = k
+        if k == n:
+            ref_hex = passes[0][1]
+    for thr, k in ((1, 16), (nproc, n)):
+        k = min(k, n)
+        run(min(thr, k), thr, 1)
+        dt = min(run(k, thr, 1)[0] for _ in range(2))
+        by_threads_iostream[str(thr)] = round(gib(k) / dt, 3)
+    all_core = by_threads[str(nproc)]
     agree = ref_hex == gpu_hex
+    quota = topo["cgroup_cpu_quota"]
     return {
-        "value": round(gib / dt, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
-        "sample": "%s over the same %d x 10 MiB chunks on %d threads, mean of 2 passes "
-                  "(%.1f core-s per pass); "
-                  "1 thread (as deployed: parts hashed serially) %.3f GiB/s on 16 chunks; "
-                  "5 threads (qsfs numtransfer default) %.3f GiB/s on 40 chunks; "
-                  "host %s, %d CPUs visible" % (
-                      what, n, threads, dt * threads, 16 * CHUNK / float(1 << 30) / dt1,
-                      40 * CHUNK / float(1 << 30) / dt5,
-                      _cpu_model(), os.cpu_count() or 0),
+        "value": all_core, "unit": "GiB/s", "cores": nproc, "kind": kind,
+        "sample": "%s, md5(std::string) form, over the same 10 MiB chunks: %s threads on "
+                  "%s chunks (best of 2 passes after a warm-up); value = all %d logical CPUs "
+                  "on all %d chunks. Host: %s, %s sockets, %s physical cores, %d logical CPUs, "
+                  "cgroup CPU quota %s" % (
+                      what, "/".join(by_threads), "/".join(str(samples[t]) for t in by_threads),
+                      nproc, n, topo["cpu_model"], topo["sockets"], topo["physical_cores"],
+                      topo["logical_cpus"], quota if quota is not None else "none"),
         "agrees_with_gpu": agree,
-        "by_threads": {"1": round(16 * CHUNK / float(1 << 30) / dt1, 3),
-                       "5": round(40 * CHUNK / float(1 << 30) / dt5, 3),
-                       str(threads): round(gib / dt, 3)},
+        "by_threads": by_threads,
+        "by_threads_iostream": by_threads_iostream,
+        "host": topo,
+        "cpu_vs_gpu": {
+            "gpu_GiBps": gpu_value, "cpu_all_cores_GiBps": all_core,
+            "cpu_1_thread_GiBps": by_threads["1"],
+            "faster_at_this_batch": "cpu" if all_core > gpu_value else "gpu",
+            "note": "at batch=512 the GPU job is 512 serial MD5 chains (one per chunk); a host "
+                    "with more cores than that ratio needs hashes the same 512 chains on its "
+                    "cores. The GPU frees those cores; it outruns them once a batch holds "
+                    "thousands of chains (config 5: 10 000 parts)"},
     }
-
-
-def _cpu_model():
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
 
 
 def _traffic_from_profiles():
@@ -137,7 +183,6 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=BATCH, help="chunks per GPU (default 512)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-always", action="store_true",
                     help="init the process group and gather digests even at world size 1 "
                          "(exercises the RCCL path on a 1-GPU box)")
@@ -145,6 +190,8 @@ def main():
                     help="N>1 rehearsal on a 1-GPU box: every rank on cuda:0, gloo digest gather")
     args = ap.parse_args()
 
+    # The bench measures the gfx950 kernels only: no CPU routing or fallback.
+    os.environ["QSMD5_BACKEND"] = "gpu"
     import torch
     import torch.distributed as dist
     import qsmd5
@@ -156,7 +203,7 @@ def main():
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
     if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU (the MD5 path has no CPU fallback)")
+        raise SystemExit("bench.py needs a GPU (it measures the gfx950 kernels)")
     if args.rehearse_gloo:
         local = 0
     torch.cuda.set_device(local)
@@ -281,10 +328,9 @@ def main():
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         host = data.cpu().numpy()
         chunks = [host[i * L:(i + 1) * L].ctypes.data for i in range(B)]
-        cb = cpu_baseline(chunks, got_hex[:B], threads)
+        cb = cpu_baseline(chunks, got_hex[:B], round(value, 3))
         result["cpu_baseline"] = cb
         if not cb["agrees_with_gpu"]:
             result["parity"] = "FAIL (cpu reference disagrees)"

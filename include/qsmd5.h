@@ -22,9 +22,18 @@
  *     -EIO); qsmd5_strerror() / qsmd5_last_error() describe failures;
  *   - digests are the 16 raw MD5 bytes (RFC 1321 byte order), identical to
  *     the reference's MD5::digest; qsmd5_hex() gives its hexdigest() text;
- *   - hashing runs on the GPU only.  There is no CPU fallback: with no usable
- *     device every hashing call fails with -ENODEV.  (The reference had no
- *     error path; callers map a failure to QSError and retry the part.)
+ *   - the backend is chosen per call: QSMD5_BACKEND=auto
+ *     (default) hashes on the CPU when its estimated time is below the GPU's
+ *     (a lone part, a few parts, tiny objects one call at a time) and on the
+ *     GPU above that break-even; "gpu" forces the gfx950 kernels (no
+ *     fallback: without a usable device every hashing call fails with
+ *     -ENODEV); "cpu" forces the library's CPU MD5.  QSMD5_FLAG_GPU_ONLY /
+ *     QSMD5_FLAG_CPU_ONLY override the environment per call.
+ *   - in auto mode a GPU failure falls back to the CPU and returns the same
+ *     digest (never an empty Content-MD5).  A sticky HIP error
+ *     (a lost GPU context) is logged once to stderr and every later call of
+ *     the process hashes on the CPU; qsmd5_get_stats reports it.
+ *     QSMD5_LOG=1 logs each call's backend, reason and size to stderr.
  *   - lengths up to 2^38 bytes per chunk; the full 64-bit MD5 length is used.
  *     The reference truncates lengths >= 4 GiB (MD5.h:53 32-bit size_type,
  *     MD5.cpp:106); set QSMD5_FLAG_REF_TRUNCATE32 to reproduce that.
@@ -83,6 +92,8 @@ typedef struct qsmd5_part {
 #define QSMD5_FLAG_NONE 0
 #define QSMD5_FLAG_REF_TRUNCATE32 1 /* hash only len mod 2^32 bytes, like MD5(std::string) */
 #define QSMD5_FLAG_ALIGNED16 2      /* device_async_ex: caller promises 16-B-aligned chunk ptrs */
+#define QSMD5_FLAG_GPU_ONLY 8       /* hash_batch_ex: gfx950 kernels only, no CPU routing/fallback */
+#define QSMD5_FLAG_CPU_ONLY 16      /* hash_batch_ex: the library's CPU MD5 only */
 #define QSMD5_FLAG_HOST 4           /* hash_batch_ex: caller promises every chunk is host memory
                                      * (pageable, pinned or registered), as qsfs's part buffers
                                      * are; skips pointer classification (otherwise one query per
@@ -200,6 +211,30 @@ QSMD5_API int qsmd5_etag_matches(const uint8_t digest[16], const char* etag);
 /* Hash [ptr, ptr+len) (host or device memory) and compare with etag:
  * 1 / 0 as above, or a negative errno. */
 QSMD5_API int qsmd5_verify_etag(const void* ptr, uint64_t len, const char* etag);
+
+/* Backend of the calling thread's last hashing call (hash_batch[_ex],
+ * hash_one, hash_parts, verify_etag): QSMD5_BACKEND_GPU, QSMD5_BACKEND_CPU,
+ * or 0 before the first call. */
+#define QSMD5_BACKEND_GPU 1
+#define QSMD5_BACKEND_CPU 2
+QSMD5_API int qsmd5_last_backend(void);
+
+/* The backend QSMD5_BACKEND=auto picks for this batch while the GPU is
+ * healthy (host-only, needs no GPU): QSMD5_BACKEND_CPU when the CPU's
+ * estimated time is the lower (QSMD5_CPU_THREADS threads, default 4, at
+ * QSMD5_CPU_GIBS GiB/s each, default 0.7), else QSMD5_BACKEND_GPU. */
+QSMD5_API int qsmd5_route(const qsmd5_chunk* chunks, size_t n, int flags);
+
+/* Process-wide backend counters since load. */
+typedef struct qsmd5_stats {
+  uint64_t gpu_batches;  /* calls hashed by the gfx950 kernels */
+  uint64_t cpu_batches;  /* calls hashed by the CPU MD5 (routed, forced or fallback) */
+  uint64_t fallbacks;    /* of those, calls whose GPU attempt failed */
+  uint64_t gpu_chunks, cpu_chunks;
+  int gpu_lost;          /* 1 once a sticky HIP error was seen: all later calls run on the CPU */
+  int reserved;
+} qsmd5_stats;
+QSMD5_API int qsmd5_get_stats(qsmd5_stats* out);
 
 /* Timing of the most recent synchronous batch on this process (ms): total
  * wall, and GPU kernel time between the first and last kernel event. */

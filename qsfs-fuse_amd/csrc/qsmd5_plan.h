@@ -157,6 +157,58 @@ inline HostPlan plan_host(const std::vector<uint64_t>& host_len, uint64_t stagin
   return P;
 }
 
+// H2D copy runs of one slice (qsmd5_runtime.cpp run_batch).  Rows k .. k+rows-1
+// of a slice's active chunks go as ONE hipMemcpy2DAsync when they have equal
+// widths, a constant source stride >= the width (and < 2^40), AND their whole
+// source span [src(k), src(k + rows - 1) + w) lies inside one allocation or
+// mapping (span_ok).  A 2-D copy reads its source as that span: across two
+// allocations it touches memory the caller never passed in.  With a pinned
+// first row HIP reads the span by DMA, and the bytes past the allocation were
+// a GPU page fault (GPUTEST_r01.json, test_gpu_fuzz seed 0: equal-length
+// chunks in a pinned pool and a pageable numpy pool).  A run whose span leaves
+// its first row's allocation is cut at the longest prefix that stays inside it
+// (span_ok is monotone in the span's end), and the rest start a new run.
+// Negative, zero (duplicates) and overlapping (< w) strides never merge.
+struct CopyRun {
+  size_t first, rows;  // rows [first, first + rows) of the slice's active chunks
+  uint64_t stride;     // source pitch of a multi-row run (0 for one row)
+};
+
+// src(k): source address of row k (column offset included); w(k): its bytes;
+// span_ok(lo, hi): [lo, hi) lies in ONE allocation or mapping.
+template <class Src, class Width, class SpanOk>
+inline std::vector<CopyRun> plan_copy_runs(size_t n, Src&& src, Width&& w, SpanOk&& span_ok) {
+  std::vector<CopyRun> runs;
+  constexpr uint64_t kMaxStride = 1ull << 40;
+  for (size_t k = 0; k < n;) {
+    const uint64_t w0 = w(k), s0 = src(k);
+    size_t rows = 1;
+    uint64_t stride = 0;
+    if (k + 1 < n && w0 > 0 && w(k + 1) == w0 && src(k + 1) > s0) {
+      const uint64_t d = src(k + 1) - s0;
+      if (d >= w0 && d < kMaxStride) {
+        rows = 2;
+        while (k + rows < n && w(k + rows) == w0 && src(k + rows) > src(k + rows - 1) &&
+               src(k + rows) - src(k + rows - 1) == d)
+          ++rows;
+        auto fits = [&](size_t r) { return span_ok(s0, s0 + (uint64_t)(r - 1) * d + w0); };
+        if (!fits(rows)) {
+          size_t good = 1, bad = rows;  // fits(1) holds: one row is the caller's own bytes
+          while (bad - good > 1) {
+            const size_t mid = good + (bad - good) / 2;
+            (fits(mid) ? good : bad) = mid;
+          }
+          rows = good;
+        }
+        if (rows > 1) stride = d;
+      }
+    }
+    runs.push_back(CopyRun{k, rows, stride});
+    k += rows;
+  }
+  return runs;
+}
+
 // Multi-GPU split of host chunks (qsmd5_runtime.cpp run_sharded): the chunks
 // (in caller order, lengths host_len) go in contiguous, byte-balanced ranges to
 // k = min(ndev, ceil(total / shard_bytes)) GPUs; a small batch stays on one

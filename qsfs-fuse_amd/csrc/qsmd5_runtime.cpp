@@ -2,9 +2,10 @@
 //
 // Owns the device, streams, descriptor/digest scratch and the host->device
 // staging ring.  Every entry point is extern "C", catches everything, and
-// reports failure as a negative errno (never an empty digest).  There is no
-// CPU hashing path: the only MD5 implementation in this library is the gfx950
-// kernel set in md5_kernels.hip.
+// reports failure as a negative errno (never an empty digest).  Hashing runs on
+// the gfx950 kernels (md5_kernels.hip) or on the library's own CPU MD5
+// (md5_cpu.h), chosen per call by size, with a CPU fallback when the GPU fails
+// ("backend routing" below).
 //
 // Host-resident batches (the qsfs case: parts sit in pooled host buffers,
 // ResourceManager.cpp:53-77) are cut into slices (a quarter of the batch,
@@ -24,6 +25,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -34,6 +36,7 @@
 #include <vector>
 
 #include "../../include/qsmd5.h"
+#include "md5_cpu.h"
 #include "md5_launch.h"
 #include "qsmd5_plan.h"
 #include "qsmd5_vma.h"
@@ -334,7 +337,7 @@ class Classifier {
       size_t size = 0;
       if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) == hipSuccess && size &&
           a - reinterpret_cast<uintptr_t>(base) < size)
-        remember(reinterpret_cast<uintptr_t>(base), size, kind, *owner);
+        remember(reinterpret_cast<uintptr_t>(base), size, kind, *owner, true);
       else
         (void)hipGetLastError();
     } else if (kind == kHostMem && ++pageable_queries_ >= maps_after_) {
@@ -342,9 +345,43 @@ class Classifier {
       auto it = std::upper_bound(vmas_.begin(), vmas_.end(), a,
                                  [](uintptr_t x, const Vma& v) { return x < v.lo; });
       if (it != vmas_.begin() && a - (it - 1)->lo < (it - 1)->hi - (it - 1)->lo)
-        remember((it - 1)->lo, (it - 1)->hi - (it - 1)->lo, kHostMem, -1);
+        remember((it - 1)->lo, (it - 1)->hi - (it - 1)->lo, kHostMem, -1, false);
     }
     return kind;
+  }
+
+  // Does [lo, hi) lie inside ONE allocation or mapping?  Decides whether rows
+  // of host chunks may go as one 2-D copy (qsmd5_plan.h plan_copy_runs), so it
+  // is exact and ignores QSMD5_FLAG_HOST: a HIP-known first row (pinned or
+  // registered) needs the span inside its exact HIP allocation, which HIP then
+  // reads by DMA; a pageable first row needs the span inside one host VMA, which
+  // HIP reads with the CPU.  The VMA cache of operator() is not used here: a
+  // registered subrange of a pageable VMA is HIP memory with a smaller range.
+  bool span_in_one(uintptr_t lo, uintptr_t hi) {
+    if (hi <= lo) return true;
+    for (int k = 0; k < used_; ++k) {
+      const Range& r = ranges_[(next_ + kRanges - 1 - k) % kRanges];
+      if (r.hip && lo - r.lo < r.size) return hi - r.lo <= r.size;
+    }
+    int owner = -1;
+    bool hip_known = false;
+    (void)classify(reinterpret_cast<const void*>(lo), &owner, &hip_known);
+    if (hip_known) {
+      hipDeviceptr_t base = nullptr;
+      size_t size = 0;
+      if (hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(lo)) != hipSuccess || !size) {
+        (void)hipGetLastError();
+        return false;
+      }
+      const uintptr_t b = reinterpret_cast<uintptr_t>(base);
+      if (lo - b >= size) return false;
+      remember(b, size, owner >= 0 ? kDeviceMem : kHostMem, owner, true);
+      return hi - b <= size;
+    }
+    if (!maps_read_) read_maps();
+    auto it = std::upper_bound(vmas_.begin(), vmas_.end(), lo,
+                               [](uintptr_t x, const Vma& v) { return x < v.lo; });
+    return it != vmas_.begin() && lo < (it - 1)->hi && hi <= (it - 1)->hi;
   }
 
  private:
@@ -355,8 +392,8 @@ class Classifier {
   struct Vma {
     uintptr_t lo, hi;
   };
-  void remember(uintptr_t lo, size_t size, MemKind kind, int owner) {
-    ranges_[next_] = Range{lo, size, kind, owner};
+  void remember(uintptr_t lo, size_t size, MemKind kind, int owner, bool hip) {
+    ranges_[next_] = Range{lo, size, kind, owner, hip};
     next_ = (next_ + 1) % kRanges;
     used_ = used_ < kRanges ? used_ + 1 : kRanges;
   }
@@ -377,6 +414,7 @@ class Classifier {
     size_t size;
     MemKind kind;
     int owner;
+    bool hip;  // an exact HIP allocation (else a host VMA)
   };
   static constexpr int kRanges = 8;
   Range ranges_[kRanges] = {};
@@ -588,7 +626,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   // (after the kernel that last used the region), then a launch on its group's
   // compute stream (so a group's columns run in order) once the copy and the
   // descriptors have landed.  Runs of equal-length chunks at a constant host
-  // stride (a file's parts) go as one 2-D copy per column.
+  // stride inside one allocation (a file's parts) go as one 2-D copy per column.
   for (size_t si = 0; si < slices.size(); ++si) {
     const qsmd5::Slice& sl = slices[si];
     const qsmd5::Group& g = groups[sl.group];
@@ -604,47 +642,41 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     const uint64_t col_off = W == kNoColumns ? 0 : (uint64_t)sl.col * W;
     uint8_t* dst = slice_base[si];
     if (trace) QS_HIP(hipEventRecord(tr[4 * si], cp));
-    for (size_t k = 0; k < sl.active && !inline_data;) {
-      const uint32_t ci = host_idx[g.first + k];
+    // Runs of equal-length rows at a constant stride inside one allocation or
+    // mapping go as one 2-D copy (qsmd5_plan.h plan_copy_runs, CPU-tested in
+    // tests/cpp/test_plan.cpp); every other row is its own copy.
+    const std::vector<qsmd5::CopyRun> runs =
+        inline_data ? std::vector<qsmd5::CopyRun>()
+                    : qsmd5::plan_copy_runs(
+                          sl.active,
+                          [&](size_t k) {
+                            return (uint64_t)reinterpret_cast<uintptr_t>(chunks[host_idx[g.first + k]].ptr) +
+                                   col_off;
+                          },
+                          [&](size_t k) { return col_bytes(len[host_idx[g.first + k]], sl.col); },
+                          [&](uint64_t lo, uint64_t hi) { return cls.span_in_one(lo, hi); });
+    for (const qsmd5::CopyRun& run : runs) {
+      const uint32_t ci = host_idx[g.first + run.first];
       const uint64_t w = col_bytes(len[ci], sl.col);
       const uint8_t* src = static_cast<const uint8_t*>(chunks[ci].ptr) + col_off;
-      size_t rows = 1;
-      int64_t stride = 0;
-      if (k + 1 < sl.active) {
-        const uint32_t c1 = host_idx[g.first + k + 1];
-        stride = static_cast<const uint8_t*>(chunks[c1].ptr) -
-                 static_cast<const uint8_t*>(chunks[ci].ptr);
-        if (len[c1] == len[ci] && stride >= (int64_t)w && stride < (1ll << 40)) {
-          while (k + rows < sl.active) {
-            const uint32_t cr = host_idx[g.first + k + rows];
-            const uint32_t cq = host_idx[g.first + k + rows - 1];
-            if (len[cr] != len[ci] || static_cast<const uint8_t*>(chunks[cr].ptr) -
-                                              static_cast<const uint8_t*>(chunks[cq].ptr) != stride)
-              break;
-            ++rows;
-          }
-        }
-      }
-      hipError_t e = hipErrorInvalidValue;
-      if (rows > 1) {
-        e = hipMemcpy2DAsync(dst, stage_bytes(w), src, (size_t)stride, w, rows,
+      hipError_t e = hipSuccess;
+      if (run.rows > 1) {
+        e = hipMemcpy2DAsync(dst, stage_bytes(w), src, (size_t)run.stride, w, run.rows,
                              hipMemcpyHostToDevice, cp);
-        // HIP checks a pinned source span against ONE allocation.  Equal-length
-        // chunks in different pinned buffers that happen to sit at a constant
-        // spacing are rejected (nothing is enqueued): copy them row by row.
+        // Belt and braces: should HIP still refuse a span inside one allocation
+        // (nothing is enqueued then), copy the rows one by one.
         if (e == hipErrorInvalidValue) {
           (void)hipGetLastError();
           e = hipSuccess;
-          for (size_t j = 0; j < rows && e == hipSuccess; ++j)
-            e = hipMemcpyAsync(dst + j * stage_bytes(w), src + (int64_t)j * stride, w,
+          for (size_t j = 0; j < run.rows && e == hipSuccess; ++j)
+            e = hipMemcpyAsync(dst + j * stage_bytes(w), src + j * run.stride, w,
                                hipMemcpyHostToDevice, cp);
         }
       } else {
         e = hipMemcpyAsync(dst, src, w, hipMemcpyHostToDevice, cp);
       }
       if (e != hipSuccess) return drain(hip_fail(e, "hipMemcpyAsync H2D"));
-      dst += rows * stage_bytes(w);
-      k += rows;
+      dst += run.rows * stage_bytes(w);
     }
     if (trace) QS_HIP(hipEventRecord(tr[4 * si + 1], cp));
     hipError_t e = hipSuccess;
@@ -985,8 +1017,26 @@ int group_commit(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], in
   return req.rc;
 }
 
+// Entry points leave the calling thread's current HIP device as they found
+// it: the runtime makes its own GPU current, and a torch or HIP thread working
+// on another GPU must not come back on ours.
+struct DeviceRestore {
+  int prev = -1;
+  DeviceRestore() {
+    if (hipGetDevice(&prev) != hipSuccess) {
+      prev = -1;
+      (void)hipGetLastError();
+    }
+  }
+  ~DeviceRestore() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
 template <class F>
 int guarded(F&& f) {
+  DeviceRestore keep;
   try {
     return f();
   } catch (const std::bad_alloc&) {
@@ -996,13 +1046,227 @@ int guarded(F&& f) {
   }
 }
 
+// ---- backend routing ---------------------------------------------------------
+// "The backend is chosen by size: CPU below a threshold, GPU
+// above" and "GPU failure falls back to CPU and returns the same digest"; §5:
+// log the backend; an env knob selects auto/cpu/gpu.
+//
+// A GPU batch costs one chain time for its longest chunk whatever its width
+// (the latency kernel's 1207 cycles per 64 B at 2.4 GHz = 0.119 GiB/s per
+// chain), plus its bytes over the host link (53.7 GiB/s measured) and ~30 us
+// of calls.  The CPU hashes each chunk as one chain too, ~6x faster per chain
+// (md5_cpu.h; 0.6-0.8 GiB/s per core), but only T = QSMD5_CPU_THREADS chains
+// at a time.  So a lone part (the reference's unchanged per-part md5() call
+// site, QSClient.cpp:369-371) is always faster on the CPU: 10 MiB in ~14 ms
+// against ~84 ms.  Equal parts of any size break even at
+//   n = (1/r_chain + ...) ~ 8.4 / (1/(T r_cpu) - 1/r_link) ~ 25 parts at T = 4,
+// and 1 KiB objects at ~30 per call.  Above that the gfx950 kernels win, and
+// win by 20-70x on whole files (batch pre-hash, §8f row 1).
+constexpr double kGpuChainGiBs = 0.119;
+constexpr double kLinkGiBs = 53.7;
+constexpr double kGpuCallMs = 0.03;
+
+enum Backend { kAuto = 0, kGpu = 1, kCpu = 2 };
+
+std::atomic<uint64_t> g_gpu_batches{0}, g_cpu_batches{0}, g_fallbacks{0};
+std::atomic<uint64_t> g_gpu_chunks{0}, g_cpu_chunks{0};
+std::atomic<bool> g_gpu_lost{false};
+thread_local int t_last_backend = 0;
+
+int requested_backend(int flags, Backend* b) {
+  if ((flags & QSMD5_FLAG_GPU_ONLY) && (flags & QSMD5_FLAG_CPU_ONLY))
+    return fail(-EINVAL, "qsmd5: QSMD5_FLAG_GPU_ONLY and QSMD5_FLAG_CPU_ONLY together");
+  if (flags & QSMD5_FLAG_GPU_ONLY) {
+    *b = kGpu;
+    return 0;
+  }
+  if (flags & QSMD5_FLAG_CPU_ONLY) {
+    *b = kCpu;
+    return 0;
+  }
+  const char* e = getenv("QSMD5_BACKEND");
+  *b = (e && !strcmp(e, "gpu")) ? kGpu : (e && !strcmp(e, "cpu")) ? kCpu : kAuto;
+  if (e && *e && *b == kAuto && strcmp(e, "auto"))
+    return fail(-EINVAL, "qsmd5: QSMD5_BACKEND must be auto, gpu or cpu");
+  return 0;
+}
+
+size_t cpu_threads() {
+  const uint64_t hw = std::max(1u, std::thread::hardware_concurrency());
+  return (size_t)std::max<uint64_t>(1, std::min<uint64_t>(hw, env_u64("QSMD5_CPU_THREADS", 4)));
+}
+
+double cpu_gibs_per_thread() {
+  const char* e = getenv("QSMD5_CPU_GIBS");
+  const double v = e && *e ? atof(e) : 0.0;
+  return v > 0 ? v : 0.7;
+}
+
+// True when the CPU is expected to finish this batch first (see above).
+bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
+  uint64_t total = 0, longest = 0;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t L = chunks[i].len;
+    if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;
+    total += L;
+    longest = std::max(longest, L);
+  }
+  const double GiB = 1073741824.0;
+  const double T = (double)cpu_threads(), rc = cpu_gibs_per_thread();
+  const double cpu_ms = 1e3 * std::max((double)longest / rc, (double)total / (T * rc)) / GiB;
+  const double gpu_ms = kGpuCallMs + 1e3 * ((double)longest / kGpuChainGiBs + (double)total / kLinkGiBs) / GiB;
+  return cpu_ms < gpu_ms;
+}
+
+// The CPU backend: every chunk on up to cpu_threads() host threads (longest
+// first, taken from a shared counter).  Device-resident chunks are first
+// copied to host memory; that needs a working HIP context.
+int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
+  std::vector<uint64_t> len(n);
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) {
+    len[i] = chunks[i].len;
+    if (flags & QSMD5_FLAG_REF_TRUNCATE32) len[i] &= 0xffffffffull;
+    if (len[i] >= kMaxChunkLen) return fail(-EINVAL, "qsmd5: chunk longer than 2^38 bytes");
+    if (len[i] && !chunks[i].ptr) return fail(-EINVAL, "qsmd5: NULL ptr with non-zero len");
+    total += len[i];
+  }
+  // Device memory cannot be read by a host core: find it (only where HIP has
+  // devices at all, and not when the caller vouches for host memory).
+  std::vector<const uint8_t*> src(n);
+  for (size_t i = 0; i < n; ++i) src[i] = static_cast<const uint8_t*>(chunks[i].ptr);
+  std::vector<std::vector<uint8_t>> copies;
+  if (!(flags & QSMD5_FLAG_HOST) && qsmd5_device_count() > 0) {
+    Classifier cls(flags, n);
+    for (size_t i = 0; i < n; ++i) {
+      int owner = -1;
+      if (!len[i] || cls(chunks[i].ptr, &owner) != kDeviceMem) continue;
+      if (g_gpu_lost.load())
+        return fail(-EIO, "qsmd5: the GPU context is lost; a device-resident chunk cannot be read");
+      copies.emplace_back(len[i]);
+      hipError_t e = hipMemcpy(copies.back().data(), chunks[i].ptr, len[i], hipMemcpyDeviceToHost);
+      if (e != hipSuccess) return hip_fail(e, "qsmd5 CPU backend: hipMemcpy D2H of a device chunk");
+      src[i] = copies.back().data();
+    }
+  }
+  std::vector<uint32_t> order(n);
+  std::iota(order.begin(), order.end(), 0u);
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len[a] > len[b]; });
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (size_t k; (k = next.fetch_add(1)) < n;) {
+      const uint32_t i = order[k];
+      qsmd5::cpu::md5(src[i], len[i], digests[i]);
+    }
+  };
+  // Threads only where they pay (a thread start costs ~20-50 us): >= 1 MiB
+  // of work per thread.
+  const size_t T = std::min<size_t>({cpu_threads(), n, (size_t)std::max<uint64_t>(1, total >> 20)});
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < T; ++t) {
+    try {
+      th.emplace_back(work);
+    } catch (...) {
+      break;  // fewer helpers: the calling thread still takes every chunk left
+    }
+  }
+  work();
+  for (auto& t : th) t.join();
+  return 0;
+}
+
+void log_call(const char* backend, const char* reason, size_t n, const qsmd5_chunk* chunks) {
+  static const bool on = env_u64("QSMD5_LOG", 0) != 0;
+  if (!on) return;
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += chunks[i].len;
+  fprintf(stderr, "qsmd5: backend=%s reason=%s chunks=%zu bytes=%llu\n", backend, reason, n,
+          (unsigned long long)total);
+}
+
+// After a failed GPU batch: is the HIP context gone for good (a sticky error
+// such as an illegal address)?  Then every later call goes to the CPU; the
+// daemon keeps producing Content-MD5s until it is restarted.
+void note_gpu_failure(int rc, bool injected_sticky) {
+  if (g_gpu_lost.load()) return;
+  bool lost = injected_sticky;
+  std::string why = injected_sticky ? "injected sticky fault (QSMD5_INJECT_GPU_FAULT=sticky)" : "";
+  if (!lost && rc == -EIO && rt().ready) {
+    hipError_t e = hipStreamQuery(primary().compute[0]);
+    if (e != hipSuccess && e != hipErrorNotReady) {
+      lost = true;
+      why = hipGetErrorString(e);
+    }
+  }
+  if (lost && !g_gpu_lost.exchange(true))
+    fprintf(stderr, "qsmd5: GPU context lost (%s); hashing on the CPU from now on -- restart the "
+            "process to use the GPU again\n", why.c_str());
+}
+
+int hash_routed(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
+  Backend b = kAuto;
+  if (int rc = requested_backend(flags, &b)) return rc;
+  const int gflags = flags & ~(QSMD5_FLAG_GPU_ONLY | QSMD5_FLAG_CPU_ONLY);
+  auto on_cpu = [&](const char* reason) {
+    log_call("cpu", reason, n, chunks);
+    const int rc = cpu_batch(chunks, n, digests, gflags);
+    if (rc == 0) {
+      t_last_backend = QSMD5_BACKEND_CPU;
+      g_cpu_batches.fetch_add(1);
+      g_cpu_chunks.fetch_add(n);
+    }
+    return rc;
+  };
+  if (b == kCpu) return on_cpu("forced");
+  if (b == kAuto) {
+    if (g_gpu_lost.load()) return on_cpu("gpu-lost");
+    if (cpu_is_faster(chunks, n, gflags)) return on_cpu("size");
+  }
+  log_call("gpu", b == kGpu ? "forced" : "size", n, chunks);
+  int rc = ensure_init();
+  bool sticky = false;
+  if (rc == 0) {
+    // QSMD5_INJECT_GPU_FAULT (tests): "1" fails every GPU batch as a HIP error
+    // would, "sticky" also marks the context lost.
+    const char* inj = getenv("QSMD5_INJECT_GPU_FAULT");
+    if (inj && *inj && strcmp(inj, "0")) {
+      sticky = !strcmp(inj, "sticky");
+      rc = fail(-EIO, "qsmd5: injected GPU fault (QSMD5_INJECT_GPU_FAULT)");
+    } else {
+      rc = group_commit(chunks, n, digests, gflags);
+    }
+  }
+  if (rc == 0) {
+    t_last_backend = QSMD5_BACKEND_GPU;
+    g_gpu_batches.fetch_add(1);
+    g_gpu_chunks.fetch_add(n);
+    return 0;
+  }
+  // Forced GPU: no fallback.  -EINVAL is the caller's error, not the GPU's.
+  if (b == kGpu || rc == -EINVAL) return rc;
+  note_gpu_failure(rc, sticky);
+  const std::string gpu_err = t_last_error;
+  const int rc2 = on_cpu("fallback");
+  if (rc2) return fail(rc2, t_last_error + " (after GPU failure: " + gpu_err + ")");
+  g_fallbacks.fetch_add(1);
+  return 0;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------------------
-// Streaming context (MD5 class): state stays on the device between updates;
-// bytes that do not fill a 64-byte block wait in `tail` on the host
-// (MD5::buffer, MD5.h:79).
+// Streaming context (MD5 class).  One stream is one serial chain, which a host
+// core runs ~6x faster than one GPU lane (the routing rule above), so under
+// QSMD5_BACKEND=auto or cpu the context hashes on the CPU (md5_cpu.h; device
+// pieces are copied to the host first).  Under QSMD5_BACKEND=gpu the state
+// stays on the device between updates; bytes that do not fill a 64-byte block
+// wait in `tail` on the host (MD5::buffer, MD5.h:79).  A GPU update that fails
+// leaves the context failed: later update/final calls return -EIO rather than
+// hash a stream with a hole in it.
 struct qsmd5_ctx {
+  bool on_cpu = false;
+  bool failed = false;
+  qsmd5::cpu::Ctx cpu;
   uint32_t* d_state = nullptr;  // 4 words
   uint8_t* d_tail = nullptr;    // 64 bytes
   uint8_t* d_seg = nullptr;     // 64 bytes: column segment descriptor, lane order {0}, spare
@@ -1079,8 +1343,7 @@ int qsmd5_hash_batch_ex(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[
     if (n == 0) return 0;
     if (!chunks || !digests) return fail(-EINVAL, "qsmd5: NULL chunks/digests");
     if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
-    if (int rc = ensure_init()) return rc;
-    return group_commit(chunks, n, digests, flags);
+    return hash_routed(chunks, n, digests, flags);
   });
 }
 
@@ -1227,6 +1490,25 @@ int qsmd5_verify_etag(const void* ptr, uint64_t len, const char* etag) {
   return qsmd5_etag_matches(d, etag);
 }
 
+int qsmd5_last_backend(void) { return t_last_backend; }
+
+int qsmd5_route(const qsmd5_chunk* chunks, size_t n, int flags) {
+  if (n && !chunks) return fail(-EINVAL, "qsmd5: NULL chunks");
+  return cpu_is_faster(chunks, n, flags) ? QSMD5_BACKEND_CPU : QSMD5_BACKEND_GPU;
+}
+
+int qsmd5_get_stats(qsmd5_stats* out) {
+  if (!out) return fail(-EINVAL, "qsmd5: NULL stats");
+  memset(out, 0, sizeof(*out));
+  out->gpu_batches = g_gpu_batches.load();
+  out->cpu_batches = g_cpu_batches.load();
+  out->fallbacks = g_fallbacks.load();
+  out->gpu_chunks = g_gpu_chunks.load();
+  out->cpu_chunks = g_cpu_chunks.load();
+  out->gpu_lost = g_gpu_lost.load() ? 1 : 0;
+  return 0;
+}
+
 int qsmd5_last_timing(double* wall_ms, double* kernel_ms) {
   Runtime& r = rt();
   std::lock_guard<std::mutex> lk(r.timing_mu);
@@ -1253,6 +1535,14 @@ int qsmd5_ctx_create(qsmd5_ctx** out) {
   return guarded([&] {
     if (!out) return fail(-EINVAL, "qsmd5: NULL out");
     *out = nullptr;
+    Backend b = kAuto;
+    if (int rc = requested_backend(0, &b)) return rc;
+    if (b != kGpu) {
+      qsmd5_ctx* c = new qsmd5_ctx;
+      c->on_cpu = true;
+      *out = c;
+      return 0;
+    }
     if (int rc = ensure_init()) return rc;
     qsmd5_ctx* c = new qsmd5_ctx;
     const uint32_t init[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
@@ -1316,12 +1606,38 @@ static int ctx_blocks(qsmd5_ctx* c, const uint8_t* p, uint64_t nblk, bool on_dev
   return 0;
 }
 
+// CPU context: host pieces directly; device pieces through a bounded host copy.
+static int ctx_update_cpu(qsmd5_ctx* c, const void* ptr, uint64_t len) {
+  int owner = -1;
+  if (qsmd5_device_count() > 0 && classify(ptr, &owner) == kDeviceMem) {
+    if (g_gpu_lost.load())
+      return fail(-EIO, "qsmd5: the GPU context is lost; a device-resident piece cannot be read");
+    constexpr uint64_t kPiece = 8ull << 20;
+    std::vector<uint8_t> buf((size_t)std::min(len, kPiece));
+    for (uint64_t off = 0; off < len; off += kPiece) {
+      const uint64_t k = std::min(kPiece, len - off);
+      QS_HIP(hipMemcpy(buf.data(), static_cast<const uint8_t*>(ptr) + off, k, hipMemcpyDeviceToHost));
+      c->cpu.update(buf.data(), k);
+    }
+    return 0;
+  }
+  c->cpu.update(ptr, len);
+  return 0;
+}
+
 int qsmd5_ctx_update(qsmd5_ctx* c, const void* ptr, uint64_t len) {
   return guarded([&] {
     if (!c) return fail(-EINVAL, "qsmd5: NULL ctx");
     if (c->finalized) return fail(-EINVAL, "qsmd5: update after final");
+    if (c->failed) return fail(-EIO, "qsmd5: an earlier update of this context failed");
     if (len == 0) return 0;
     if (!ptr) return fail(-EINVAL, "qsmd5: NULL ptr with non-zero len");
+    if (c->on_cpu) {
+      // a device piece copied only in part would leave a hole: fail the context
+      const int rc = ctx_update_cpu(c, ptr, len);
+      if (rc) c->failed = true;
+      return rc;
+    }
     if (int rc = ensure_init()) return rc;
     std::lock_guard<std::mutex> lk(primary().mu);
     int owner = -1;
@@ -1331,6 +1647,15 @@ int qsmd5_ctx_update(qsmd5_ctx* c, const void* ptr, uint64_t len) {
                                ", not on the primary bound GPU");
     const uint8_t* p = static_cast<const uint8_t*>(ptr);
     uint64_t left = len;
+    // From here a failure leaves d_state, tail and total out of step: mark the
+    // context failed (every exit below that returns nonzero passes here).
+    struct FailOnError {
+      qsmd5_ctx* c;
+      bool ok = false;
+      ~FailOnError() {
+        if (!ok) c->failed = true;
+      }
+    } guard{c};
     c->total += len;
     if (c->tail_len) {
       const uint32_t take = (uint32_t)std::min<uint64_t>(64 - c->tail_len, left);
@@ -1361,6 +1686,7 @@ int qsmd5_ctx_update(qsmd5_ctx* c, const void* ptr, uint64_t len) {
       }
       c->tail_len = (uint32_t)left;
     }
+    guard.ok = true;
     return 0;
   });
 }
@@ -1368,6 +1694,11 @@ int qsmd5_ctx_update(qsmd5_ctx* c, const void* ptr, uint64_t len) {
 int qsmd5_ctx_final(qsmd5_ctx* c, uint8_t digest[16]) {
   return guarded([&] {
     if (!c || !digest) return fail(-EINVAL, "qsmd5: NULL ctx/digest");
+    if (c->failed) return fail(-EIO, "qsmd5: an earlier update of this context failed");
+    if (!c->finalized && c->on_cpu) {
+      c->cpu.final(c->digest);
+      c->finalized = true;
+    }
     if (!c->finalized) {
       if (int rc = ensure_init()) return rc;
       std::lock_guard<std::mutex> lk(primary().mu);

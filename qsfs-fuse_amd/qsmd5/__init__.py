@@ -8,9 +8,12 @@ __graft_entry__ use it.  It mirrors the reference interface names:
   MD5().update(b).finalize().hexdigest()   class MD5                MD5.h:51-93
 
 plus the batch entry points the reference lacks (hash_batch, hash_parts,
-hash_device).  Hashing runs on the GPU only: if the library is missing this
-module raises on import-time use (``lib()``), and without a GPU every hashing
-call raises ``Md5Error`` with -ENODEV -- there is no CPU fallback.
+hash_device).  If the library is missing this module raises on first use
+(``lib()``).  The library picks the backend per call (QSMD5_BACKEND =
+auto | gpu | cpu, or FLAG_GPU_ONLY / FLAG_CPU_ONLY): under "gpu" every hash
+runs on the gfx950 kernels and, without a GPU, raises ``Md5Error`` with
+-ENODEV; under "auto" small calls and GPU failures are hashed by the
+library's own CPU MD5 (``stats()`` / ``last_backend()`` say which ran).
 """
 import ctypes
 import errno
@@ -20,7 +23,8 @@ __all__ = [
     "Md5Error", "lib", "lib_path", "hexdigest", "md5", "md5_stream", "MD5", "hash_batch",
     "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
     "alloc_pinned", "free_pinned", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
-    "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST",
+    "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST", "FLAG_GPU_ONLY",
+    "FLAG_CPU_ONLY", "stats", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -39,6 +43,17 @@ class Md5Error(RuntimeError):
 
 class qsmd5_chunk(ctypes.Structure):
     _fields_ = [("ptr", ctypes.c_void_p), ("len", ctypes.c_uint64)]
+
+
+class Stats(ctypes.Structure):
+    """qsmd5_stats: process-wide backend counters."""
+    _fields_ = [("gpu_batches", ctypes.c_uint64), ("cpu_batches", ctypes.c_uint64),
+                ("fallbacks", ctypes.c_uint64), ("gpu_chunks", ctypes.c_uint64),
+                ("cpu_chunks", ctypes.c_uint64), ("gpu_lost", ctypes.c_int),
+                ("reserved", ctypes.c_int)]
+
+    def asdict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
 class Part(ctypes.Structure):
@@ -106,6 +121,9 @@ def lib():
                                             c_u8p]),
         "qsmd5_etag_matches": (ctypes.c_int, [c_u8p, ctypes.c_char_p]),
         "qsmd5_verify_etag": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p]),
+        "qsmd5_last_backend": (ctypes.c_int, []),
+        "qsmd5_route": (ctypes.c_int, [ctypes.POINTER(qsmd5_chunk), ctypes.c_size_t, ctypes.c_int]),
+        "qsmd5_get_stats": (ctypes.c_int, [ctypes.POINTER(Stats)]),
         "qsmd5_last_timing": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]),
         "qsmd5_synth_fill_lcg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
@@ -144,6 +162,33 @@ def kernel_choice(n, flags=0):
 FLAG_REF_TRUNCATE32 = 1
 FLAG_ALIGNED16 = 2
 FLAG_HOST = 4  # every chunk is host memory: skip the per-chunk pointer query
+FLAG_GPU_ONLY = 8  # gfx950 kernels only: no CPU routing or fallback
+FLAG_CPU_ONLY = 16  # the library's CPU MD5 only
+BACKEND_GPU = 1
+BACKEND_CPU = 2
+
+
+def stats():
+    """Process-wide backend counters (qsmd5_get_stats) as a dict."""
+    st = Stats()
+    _check(lib().qsmd5_get_stats(ctypes.byref(st)), "qsmd5_get_stats")
+    return st.asdict()
+
+
+def route(lengths, flags=0):
+    """Backend (BACKEND_CPU / BACKEND_GPU) that QSMD5_BACKEND=auto picks for a
+    batch of chunks of these lengths (host logic; no data is read)."""
+    n = len(lengths)
+    arr = (qsmd5_chunk * max(n, 1))()
+    for i, L in enumerate(lengths):
+        arr[i].ptr = 1 if L else 0
+        arr[i].len = L
+    return lib().qsmd5_route(arr, n, flags)
+
+
+def last_backend():
+    """BACKEND_GPU / BACKEND_CPU of this thread's last hashing call (0: none)."""
+    return lib().qsmd5_last_backend()
 
 
 def hexdigest(digest):
@@ -198,7 +243,7 @@ def _as_chunk(buf, keep):
 
 
 def hash_batch(buffers, flags=0):
-    """MD5 of every buffer (host or device), one GPU batch -> list of 16-byte digests."""
+    """MD5 of every buffer (host or device), one batch -> list of 16-byte digests."""
     bufs = list(buffers)
     n = len(bufs)
     if n == 0:

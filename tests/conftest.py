@@ -21,9 +21,16 @@ for p in (ROOT, os.path.join(ROOT, "qsfs-fuse_amd"), os.path.join(ROOT, "tests")
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# Parity tests measure the gfx950 kernels, never the library's CPU backend:
+# every test (and every subprocess it starts) runs with QSMD5_BACKEND=gpu
+# unless it sets the backend itself, and the `gpu_only_backend` fixture below
+# fails any -m gpu test during which the CPU backend hashed anything.
+os.environ["QSMD5_BACKEND"] = "gpu"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device)")
+    config.addinivalue_line("markers", "cpu_backend: exercises the library's CPU routing/fallback")
 
 
 def _ensure_built():
@@ -47,3 +54,18 @@ def load_golden(name):
 @pytest.fixture(scope="session")
 def golden():
     return load_golden
+
+
+@pytest.fixture(autouse=True)
+def gpu_only_backend(request):
+    """In -m gpu tests, the CPU backend must not have hashed a single call
+    (tests of the routing and fallback opt out with @pytest.mark.cpu_backend)."""
+    if request.node.get_closest_marker("gpu") is None or \
+            request.node.get_closest_marker("cpu_backend") is not None:
+        yield
+        return
+    import qsmd5
+    before = qsmd5.stats()["cpu_batches"]
+    yield
+    after = qsmd5.stats()["cpu_batches"]
+    assert after == before, "the CPU backend hashed %d call(s) in a GPU parity test" % (after - before)

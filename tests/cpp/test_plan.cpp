@@ -152,6 +152,134 @@ static void check_shards(const std::vector<uint64_t>& len, size_t ndev, uint64_t
   }
 }
 
+// 2-D copy runs (plan_copy_runs).  `allocs` are disjoint [lo, hi) ranges; a
+// span is ok only inside one of them.  The runs must cover rows 0..n-1 once,
+// in order; a multi-row run must have equal widths, the constant positive
+// stride of its rows, stride >= width, and its whole source span inside ONE
+// allocation (the GPUTEST_r01 fault was a span from a pinned pool into a
+// pageable one); and a run may not stop where the next row could have joined.
+struct Alloc {
+  uint64_t lo, hi;
+};
+static int span_in(const std::vector<Alloc>& a, uint64_t lo, uint64_t hi) {
+  for (size_t i = 0; i < a.size(); ++i)
+    if (lo >= a[i].lo && lo < a[i].hi) return hi <= a[i].hi ? (int)i : -1;
+  return -1;
+}
+static void check_runs(const std::vector<uint64_t>& src, const std::vector<uint64_t>& w,
+                       const std::vector<Alloc>& allocs, const char* what, size_t* multi = nullptr) {
+  const size_t n = src.size();
+  size_t span_calls = 0;
+  const std::vector<CopyRun> runs = plan_copy_runs(
+      n, [&](size_t k) { return src[k]; }, [&](size_t k) { return w[k]; },
+      [&](uint64_t lo, uint64_t hi) {
+        ++span_calls;
+        return span_in(allocs, lo, hi) >= 0;
+      });
+  size_t next = 0;
+  for (const CopyRun& r : runs) {
+    CHECK(r.first == next && r.rows >= 1, "%s: run at %zu rows %zu, expected start %zu", what,
+          r.first, r.rows, next);
+    next = r.first + r.rows;
+    if (r.rows > 1) {
+      if (multi) ++*multi;
+      CHECK(r.stride >= w[r.first] && r.stride > 0, "%s: stride %llu < width %llu", what,
+            (unsigned long long)r.stride, (unsigned long long)w[r.first]);
+      for (size_t j = 1; j < r.rows; ++j) {
+        CHECK(w[r.first + j] == w[r.first], "%s: unequal widths in a run", what);
+        CHECK(src[r.first + j] == src[r.first] + j * r.stride, "%s: row %zu off the stride", what,
+              r.first + j);
+      }
+      const uint64_t end = src[r.first] + (r.rows - 1) * r.stride + w[r.first];
+      CHECK(span_in(allocs, src[r.first], end) >= 0, "%s: run at %zu spans allocations", what,
+            r.first);
+    } else {
+      CHECK(r.stride == 0, "%s: one-row run with a stride", what);
+    }
+    const size_t nx = r.first + r.rows;  // maximality
+    if (nx < n && r.rows >= 1 && w[nx] == w[r.first] && w[nx] > 0 && src[nx] > src[nx - 1]) {
+      const uint64_t d = src[nx] - src[nx - 1];
+      const bool same = r.rows > 1 ? d == r.stride : d >= w[r.first] && d < (1ull << 40);
+      const uint64_t end = src[nx] + w[nx];
+      CHECK(!(same && span_in(allocs, src[r.first], end) >= 0), "%s: run at %zu stops early at %zu",
+            what, r.first, nx);
+    }
+  }
+  CHECK(next == n, "%s: runs cover %zu of %zu rows", what, next, n);
+  CHECK(span_calls <= 2 * runs.size() * 64 + 1, "%s: %zu span checks for %zu runs", what, span_calls,
+        runs.size());
+}
+
+static int run_copy_run_cases(std::mt19937_64& rng) {
+  int cases = 0;
+  const uint64_t MiB = 1ull << 20;
+  // The seed-0 shape: equal-length chunks, one in a pinned pool, the next in a
+  // pageable pool at a higher address with unmapped memory between them, at
+  // both orders, and equal-length pairs in two pinned pools.
+  for (uint64_t L : {55ull, 88ull, 4095ull, 1ull << 20}) {
+    const std::vector<Alloc> two = {{0x10000000, 0x10000000 + 24 * MiB},
+                                    {0x7f0000000000, 0x7f0000000000 + 24 * MiB}};
+    size_t multi = 0;
+    check_runs({two[0].lo + 100, two[1].lo + 100}, {L, L}, two, "pinned -> pageable", &multi);
+    check_runs({two[0].lo + 100, two[1].lo + 100, two[1].lo + 100 + (two[1].lo - two[0].lo)}, {L, L, L},
+               two, "stride continues past the second pool", &multi);
+    CHECK(multi == 0, "cross-allocation pairs merged (L=%llu)", (unsigned long long)L);
+    cases += 2;
+  }
+  {  // a file's parts in one buffer: one run; the same rows split over two
+     // adjacent pools (no gap): one run per pool
+    std::vector<uint64_t> src, w;
+    const std::vector<Alloc> one = {{1 << 30, (1ull << 30) + 64 * 10 * MiB}};
+    for (int i = 0; i < 64; ++i) src.push_back(one[0].lo + i * 10 * MiB), w.push_back(10 * MiB);
+    size_t multi = 0;
+    check_runs(src, w, one, "file parts", &multi);
+    CHECK(multi == 1, "file parts: %zu runs, want 1", multi);
+    const std::vector<Alloc> split = {{1 << 30, (1ull << 30) + 40 * 10 * MiB},
+                                      {(1ull << 30) + 40 * 10 * MiB, (1ull << 30) + 64 * 10 * MiB}};
+    multi = 0;
+    check_runs(src, w, split, "parts over two adjacent pools", &multi);
+    CHECK(multi == 2, "two pools: %zu runs, want 2", multi);
+    cases += 2;
+  }
+  {  // negative, zero and overlapping strides never merge
+    const std::vector<Alloc> one = {{4096, 1ull << 32}};
+    size_t multi = 0;
+    check_runs({1 << 20, (1 << 20) - 4096, (1 << 20) - 8192}, {1000, 1000, 1000}, one, "negative", &multi);
+    check_runs({1 << 20, 1 << 20, 1 << 20}, {1000, 1000, 1000}, one, "duplicates", &multi);
+    check_runs({1 << 20, (1 << 20) + 500, (1 << 20) + 1000}, {1000, 1000, 1000}, one, "overlap", &multi);
+    CHECK(multi == 0, "negative/zero/overlapping strides merged");
+    cases += 3;
+  }
+  for (int t = 0; t < 400; ++t) {  // random pools, positions and widths
+    std::vector<Alloc> allocs;
+    uint64_t base = 1 << 20;
+    const int na = 1 + (int)(rng() % 5);
+    for (int a = 0; a < na; ++a) {
+      const uint64_t size = (1 + rng() % 64) * 4096;
+      if (rng() % 2) base += (1 + rng() % 8) * 4096;  // a gap, or adjacent pools
+      allocs.push_back({base, base + size});
+      base += size;
+    }
+    const size_t n = 1 + rng() % 60;
+    std::vector<uint64_t> src(n), w(n);
+    const uint64_t W = 1 + rng() % 3000;
+    const uint64_t stride = W + rng() % 2000;
+    uint64_t p = allocs[0].lo + rng() % 512;
+    for (size_t k = 0; k < n; ++k) {
+      w[k] = rng() % 8 ? W : 1 + rng() % 3000;
+      if (rng() % 6 == 0) {  // jump into a random pool
+        const Alloc& a = allocs[rng() % allocs.size()];
+        p = a.lo + rng() % (a.hi - a.lo);
+      }
+      src[k] = p;
+      p += rng() % 10 ? stride : rng() % 9000;
+    }
+    check_runs(src, w, allocs, "random");
+    ++cases;
+  }
+  return cases;
+}
+
 int main() {
   const uint64_t MiB = 1ull << 20, GiB = 1ull << 30;
   std::mt19937_64 rng(1234);
@@ -219,6 +347,7 @@ int main() {
           ++cases;
         }
   }
+  cases += run_copy_run_cases(rng);
   printf("plan %s %d cases\n", fails ? "FAIL" : "ok", cases);
   return fails ? 1 : 0;
 }

@@ -1,0 +1,180 @@
+"""The library's CPU backend (qsfs-fuse_amd/csrc/md5_cpu.h) and the routing
+around it, on the CPU (no GPU needed).
+
+SURVEY.md §8b: "The backend is chosen by size: CPU below a threshold, GPU
+above" and "GPU failure falls back to CPU and returns the same digest"; §5:
+an env knob selects auto/cpu/gpu and the backend is logged.  This CPU MD5 is
+product code inside libqsmd5.so, so before it may answer for the GPU it is
+pinned here against every committed golden fixture (produced by the
+reference's own MD5.cpp, tests/golden/make_golden.py), exactly as the oracle
+is in test_oracle.py.  The oracle itself is only the fixture generator's
+restatement: libqsmd5.so never links or loads it (checked below).
+
+Everything here goes through the C-ABI with QSMD5_FLAG_CPU_ONLY or
+QSMD5_BACKEND=cpu/auto; without a GPU, auto mode takes the fallback path.
+"""
+import ctypes
+import errno
+import os
+import subprocess
+
+import pytest
+
+import qsmd5
+from conftest import ROOT
+from oracle_util import lcg_bytes
+
+CPU = qsmd5.FLAG_CPU_ONLY
+
+
+def _hex_all(chunks, flags=CPU):
+    return [d.hex() for d in qsmd5.hash_batch(chunks, flags=flags)]
+
+
+def test_rfc1321(golden):
+    for c in golden("rfc1321.json")["cases"]:
+        assert _hex_all([c["text"].encode()]) == [c["md5"]]
+
+
+def test_lcg_lengths_all_padding_edges(golden):
+    g = golden("lcg_lengths.json")
+    big = max(c["len"] for c in g["cases"])
+    data = lcg_bytes(g["seed"], big)
+    addr = ctypes.addressof(data)
+    got = _hex_all([(addr, c["len"]) for c in g["cases"]])
+    assert got == [c["md5"] for c in g["cases"]]
+    # unaligned starts: the same bytes at offsets 1..7 hash the same
+    for off in range(1, 8):
+        buf = (ctypes.c_uint8 * (4096 + 8))()
+        ctypes.memmove(ctypes.addressof(buf) + off, addr, 4096)
+        assert _hex_all([(ctypes.addressof(buf) + off, 4096)]) == \
+            [c["md5"] for c in g["cases"] if c["len"] == 4096]
+
+
+def test_stream_pieces_class(golden, monkeypatch):
+    """The MD5 class (qsmd5_ctx) under QSMD5_BACKEND=cpu, update() in pieces."""
+    monkeypatch.setenv("QSMD5_BACKEND", "cpu")
+    g = golden("stream_pieces.json")
+    data = lcg_bytes(g["seed"], g["len"])
+    base = ctypes.addressof(data)
+    for case in g["cases"]:
+        h = qsmd5.MD5()
+        off = 0
+        for cut in case["cuts"]:
+            h.update((base + off, cut))
+            off += cut
+        assert h.finalize().hexdigest() == case["md5"], case["cuts"][:4]
+        assert h.hexdigest() == case["md5"]
+
+
+def test_ragged_and_sweep(golden):
+    g = golden("ragged.json")
+    bufs = [lcg_bytes(7000 + i, L) for i, L in enumerate(g["lengths"])]
+    assert _hex_all([(ctypes.addressof(b), L) for b, L in zip(bufs, g["lengths"])]) == g["md5"]
+    del bufs
+    for s in g["sweep"]:
+        L = s["mib"] << 20
+        bufs = [lcg_bytes(s["seed0"] + i, L) for i in range(len(s["md5"]))]
+        assert _hex_all([(ctypes.addressof(b), L) for b in bufs]) == s["md5"], s["mib"]
+
+
+def test_batch_10mib_prefix(golden):
+    g = golden("batch_10MiB.json")
+    bufs = [lcg_bytes(12345 + i, g["len"]) for i in range(24)]
+    assert _hex_all([(ctypes.addressof(b), g["len"]) for b in bufs]) == g["md5"][:24]
+
+
+def test_truncate32(golden):
+    """>= 4 GiB: full RFC 1321 length by default; QSMD5_FLAG_REF_TRUNCATE32
+    reproduces the reference's 32-bit size_type (MD5.h:53, MD5.cpp:106)."""
+    g = golden("truncate32.json")
+    data = lcg_bytes(g["seed"], g["len"])
+    a = ctypes.addressof(data)
+    assert _hex_all([(a, g["len"])]) == [g["full_md5"]]
+    assert _hex_all([(a, g["len"])], CPU | qsmd5.FLAG_REF_TRUNCATE32) == [g["reference_md5"]]
+
+
+def test_auto_mode_without_gpu_falls_back(monkeypatch):
+    """No GPU here: auto mode still returns the digest (the fallback path) and
+    says so; forced GPU fails loudly with -ENODEV."""
+    if qsmd5.device_count() > 0:
+        pytest.skip("GPU present")
+    monkeypatch.setenv("QSMD5_BACKEND", "auto")
+    big = lcg_bytes(12345, 10 << 20)
+    many = [(ctypes.addressof(big) + i * (256 << 10), 256 << 10) for i in range(40)]
+    before = qsmd5.stats()
+    assert qsmd5.route([256 << 10] * 40) == qsmd5.BACKEND_GPU  # GPU would be picked ...
+    got = qsmd5.hash_batch(many)  # ... fails (no device), and the CPU answers
+    assert got == qsmd5.hash_batch(many, flags=CPU)
+    assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
+    after = qsmd5.stats()
+    assert after["fallbacks"] == before["fallbacks"] + 1
+    assert qsmd5.md5("abc") == "900150983cd24fb0d6963f7d28e17f72"  # routed by size
+    with pytest.raises(qsmd5.Md5Error) as e:
+        qsmd5.hash_batch(many, flags=qsmd5.FLAG_GPU_ONLY)
+    assert e.value.code == -errno.ENODEV
+    with pytest.raises(qsmd5.Md5Error) as e:
+        qsmd5.hash_batch([b"x"], flags=qsmd5.FLAG_GPU_ONLY | CPU)
+    assert e.value.code == -errno.EINVAL
+
+
+def test_bad_backend_name(monkeypatch):
+    monkeypatch.setenv("QSMD5_BACKEND", "fpga")
+    with pytest.raises(qsmd5.Md5Error) as e:
+        qsmd5.hash_one(b"abc")
+    assert e.value.code == -errno.EINVAL
+
+
+def test_routing_rule(monkeypatch):
+    """Size routing (qsmd5_route): a lone part of any size goes to the CPU (the
+    unchanged per-part md5() call site, QSClient.cpp:369-371); whole files'
+    parts and large object batches go to the GPU; the break-even moves with
+    QSMD5_CPU_THREADS as the cost model says."""
+    monkeypatch.delenv("QSMD5_CPU_THREADS", raising=False)
+    monkeypatch.delenv("QSMD5_CPU_GIBS", raising=False)
+    C, G = qsmd5.BACKEND_CPU, qsmd5.BACKEND_GPU
+    MiB = 1 << 20
+    for L in (0, 1, 1024, 10 * MiB, 64 * MiB, 4 << 30):
+        assert qsmd5.route([L]) == C, L
+    assert qsmd5.route([10 * MiB] * 512) == G  # BASELINE config 2
+    assert qsmd5.route([10 * MiB] * 10000) == G  # config 5
+    assert qsmd5.route([1024] * (1 << 20)) == G  # many small objects
+
+    def break_even(L, lo=1, hi=1 << 16):
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            lo, hi = (mid, hi) if qsmd5.route([L] * mid) == C else (lo, mid)
+        return hi  # first batch size that goes to the GPU
+
+    n4 = break_even(10 * MiB)
+    assert 15 <= n4 <= 40, n4
+    monkeypatch.setenv("QSMD5_CPU_THREADS", "1")
+    n1 = break_even(10 * MiB)
+    assert n1 < n4 and 4 <= n1 <= 10, n1
+    # routing is monotone in the batch size for equal parts
+    monkeypatch.delenv("QSMD5_CPU_THREADS")
+    seq = [qsmd5.route([MiB] * n) for n in range(1, 200)]
+    assert seq == sorted(seq, key=lambda b: b == G)
+
+
+def test_log_names_the_backend(tmp_path):
+    """QSMD5_LOG=1 logs each call's backend, reason and size."""
+    code = ("import sys; sys.path.insert(0, %r); import qsmd5; "
+            "qsmd5.hash_batch([b'abc'] * 3, flags=qsmd5.FLAG_CPU_ONLY)"
+            % os.path.join(ROOT, "qsfs-fuse_amd"))
+    env = dict(os.environ, QSMD5_LOG="1")
+    out = subprocess.run(["python", "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "qsmd5: backend=cpu reason=forced chunks=3 bytes=9" in out.stderr
+
+
+def test_product_library_does_not_carry_the_oracle():
+    """The CPU backend is the library's own code: libqsmd5.so neither links
+    the oracle nor exports or contains its symbols."""
+    so = qsmd5.lib_path()
+    needed = subprocess.run(["readelf", "-d", so], capture_output=True, text=True).stdout
+    assert "md5_oracle" not in needed and "ref_md5" not in needed
+    syms = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True).stdout
+    assert "oracle_" not in syms and "ref_md5" not in syms
+    allsyms = subprocess.run(["nm", so], capture_output=True, text=True).stdout
+    assert "oracle_md5" not in allsyms

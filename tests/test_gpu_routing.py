@@ -1,0 +1,160 @@
+"""Backend routing and GPU-failure fallback on the MI355X.
+
+QSMD5_BACKEND=auto sends a batch to the CPU when the CPU's estimated time is
+the lower (a lone part, a few parts) and to the gfx950 kernels above the
+break-even; a GPU failure falls back to the library's CPU MD5 and returns the
+same digest; a lost GPU context sends every later call to the CPU.  Failures
+are injected with QSMD5_INJECT_GPU_FAULT (no real fault is provoked on the
+box).  Every digest is checked against the oracle.
+"""
+import ctypes
+import os
+import statistics
+import subprocess
+import sys
+import time
+
+import pytest
+
+import qsmd5
+from conftest import ROOT
+from oracle_util import lcg_bytes, md5_many
+
+torch = pytest.importorskip("torch")
+pytestmark = [pytest.mark.gpu, pytest.mark.cpu_backend]
+
+MiB = 1 << 20
+
+
+@pytest.fixture
+def auto(monkeypatch):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.setenv("QSMD5_BACKEND", "auto")
+    monkeypatch.delenv("QSMD5_INJECT_GPU_FAULT", raising=False)
+    assert qsmd5.lib().qsmd5_init(0) == 0
+
+
+def _batch(n, L, seed=500):
+    bufs = [lcg_bytes(seed + i, L) for i in range(n)]
+    return bufs, [(ctypes.addressof(b), L) for b in bufs]
+
+
+def test_break_even_batches_take_the_gpu(auto):
+    _, chunks = _batch(64, MiB)
+    assert qsmd5.route([MiB] * 64) == qsmd5.BACKEND_GPU
+    s0 = qsmd5.stats()
+    assert qsmd5.hash_batch(chunks) == md5_many(chunks)
+    assert qsmd5.last_backend() == qsmd5.BACKEND_GPU
+    assert qsmd5.stats()["gpu_batches"] == s0["gpu_batches"] + 1
+
+
+def test_lone_part_goes_to_the_cpu_and_beats_the_reference(auto):
+    """The unchanged per-part call site (QSClient.cpp:369-371 -> md5(iostream),
+    MD5.cpp:341-349) on one 10 MiB part: routed to the CPU, and no slower than
+    the reference's md5(iostream) on this host (oracle/_ref, when built)."""
+    data = lcg_bytes(12345, 10 * MiB)
+    addr = ctypes.addressof(data)
+    times = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        d = qsmd5.hash_one((addr, 10 * MiB))
+        times.append(time.perf_counter() - t0)
+        assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
+    assert d.hex() == "302bec822b27cea263612fb3f76fa34b"
+    ours = statistics.median(times)
+    ref_so = os.path.join(ROOT, "oracle", "_ref", "libref_md5.so")
+    if not os.path.exists(ref_so):
+        pytest.skip("reference build absent; ours %.1f ms" % (ours * 1e3))
+    R = ctypes.CDLL(ref_so)
+    R.ref_md5_iostream.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_char_p]
+    rt = []
+    out = ctypes.create_string_buffer(33)
+    for _ in range(5):
+        t0 = time.perf_counter()
+        R.ref_md5_iostream(addr, 10 * MiB, out)
+        rt.append(time.perf_counter() - t0)
+    ref = statistics.median(rt)
+    print("lone 10 MiB part: library %.2f ms (CPU route), reference md5(iostream) %.2f ms"
+          % (ours * 1e3, ref * 1e3))
+    assert out.value.decode() == "302bec822b27cea263612fb3f76fa34b"
+    assert ours <= ref * 1.05
+
+
+def test_injected_gpu_fault_falls_back_with_identical_digests(auto, monkeypatch):
+    host_bufs, host = _batch(48, MiB)
+    dev = torch.empty(16 * MiB, dtype=torch.uint8, device="cuda")
+    qsmd5.synth_fill_lcg(dev.data_ptr(), MiB, MiB, 900, 16, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    dchunks = [(dev.data_ptr() + i * MiB, MiB) for i in range(16)]
+    dhost = dev.cpu().numpy()
+    want = md5_many(host) + md5_many([(dhost.ctypes.data + i * MiB, MiB) for i in range(16)])
+    monkeypatch.setenv("QSMD5_INJECT_GPU_FAULT", "1")
+    s0 = qsmd5.stats()
+    assert qsmd5.hash_batch(host + dchunks) == want  # device chunks come back by D2H
+    assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
+    s1 = qsmd5.stats()
+    assert s1["fallbacks"] == s0["fallbacks"] + 1 and not s1["gpu_lost"]
+    # forced GPU: the failure is returned, never a digest
+    with pytest.raises(qsmd5.Md5Error):
+        qsmd5.hash_batch(host, flags=qsmd5.FLAG_GPU_ONLY)
+    monkeypatch.delenv("QSMD5_INJECT_GPU_FAULT")
+    assert qsmd5.hash_batch(host + dchunks) == want  # a transient failure: the GPU again
+    assert qsmd5.last_backend() == qsmd5.BACKEND_GPU
+
+
+_STICKY = r"""
+import ctypes, sys
+sys.path[:0] = [%(pkg)r, %(tests)r]
+import torch, qsmd5
+from oracle_util import lcg_bytes, md5_many
+bufs = [lcg_bytes(77 + i, 1 << 20) for i in range(64)]
+chunks = [(ctypes.addressof(b), 1 << 20) for b in bufs]
+want = md5_many(chunks)
+import os
+os.environ["QSMD5_INJECT_GPU_FAULT"] = "sticky"
+assert qsmd5.hash_batch(chunks) == want
+del os.environ["QSMD5_INJECT_GPU_FAULT"]
+st = qsmd5.stats()
+assert st["gpu_lost"] == 1 and st["fallbacks"] == 1, st
+assert qsmd5.hash_batch(chunks) == want  # GPU lost: straight to the CPU
+assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
+assert qsmd5.stats()["fallbacks"] == 1
+dev = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+try:
+    qsmd5.hash_batch([dev])
+    raise SystemExit("a device chunk was hashed after the context was lost")
+except qsmd5.Md5Error as e:
+    assert e.code == -5, e
+print("STICKY_OK")
+"""
+
+
+def test_lost_gpu_context_sends_every_later_call_to_the_cpu(auto):
+    code = _STICKY % {"pkg": os.path.join(ROOT, "qsfs-fuse_amd"), "tests": os.path.join(ROOT, "tests")}
+    env = dict(os.environ, QSMD5_BACKEND="auto")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "STICKY_OK" in out.stdout
+    assert "qsmd5: GPU context lost" in out.stderr  # logged once
+    assert out.stderr.count("qsmd5: GPU context lost") == 1
+
+
+def test_streaming_class_in_auto_mode_reads_device_pieces(auto):
+    """Under auto the MD5 class hashes on the CPU (one stream = one chain);
+    device pieces are copied back first.  Same digest as the oracle."""
+    L = 3 * MiB + 17
+    dev = torch.empty(L, dtype=torch.uint8, device="cuda")
+    qsmd5.synth_fill_lcg(dev.data_ptr(), L, L, 4242, 1, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    host = dev.cpu().numpy()
+    h = qsmd5.MD5()
+    cuts = [1, 63, 64, 65, MiB, 2 * MiB - 193 + 17]
+    off = 0
+    for i, c in enumerate(cuts):
+        src = dev.data_ptr() if i % 2 else host.ctypes.data
+        h.update((src + off, c))
+        off += c
+    assert off == L
+    assert h.finalize().digest() == md5_many([(host.ctypes.data, L)])[0]

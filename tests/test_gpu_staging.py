@@ -1,0 +1,166 @@
+"""Host staging across allocations: the GPUTEST_r01 illegal-memory-access case.
+
+Round 1's driver run faulted the GPU in test_gpu_fuzz seed 0: equal-length
+host chunks sitting in two different allocations (a pinned pool and a pageable
+numpy pool) were sent as ONE hipMemcpy2DAsync whose source span ran from the
+first allocation through unmapped memory into the second.  With a pinned first
+row HIP reads that span by DMA, and the bytes between the allocations faulted.
+
+The runtime now forms a 2-D copy only when the whole span lies inside one
+allocation or mapping (qsmd5_plan.h plan_copy_runs; CPU-tested by
+tests/cpp/test_plan.cpp).  These tests rebuild the failing shape on purpose,
+deterministically: a pageable mapping placed at a chosen address above or
+below a pinned buffer, with an unmapped gap between, so equal-length chunks in
+the two sit at a constant positive stride across the gap.  Every digest is
+checked against the oracle.
+"""
+import ctypes
+import mmap
+import os
+
+import numpy as np
+import pytest
+
+import qsmd5
+from oracle_util import md5_many
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+SIZE = 8 << 20
+GAP = 2 << 20
+LENGTHS = [55, 88, 4095, 4096, (256 << 10) + 7, 1 << 20]
+
+_libc = ctypes.CDLL(None, use_errno=True)
+_libc.mmap.restype = ctypes.c_void_p
+_libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                       ctypes.c_long]
+_libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+_libc.mprotect.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+MAP_FIXED_NOREPLACE = 0x100000
+MAP_FAILED = ctypes.c_void_p(-1).value
+
+
+def _map_at(addr, size):
+    """Anonymous pageable mapping at exactly `addr`, or None."""
+    p = _libc.mmap(addr, size, mmap.PROT_READ | mmap.PROT_WRITE,
+                   mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS | MAP_FIXED_NOREPLACE, -1, 0)
+    if p in (None, MAP_FAILED):
+        return None
+    if p != addr:  # an old kernel took it as a hint only
+        _libc.munmap(p, size)
+        return None
+    return p
+
+
+def _pageable_near(pinned, above):
+    """A pageable mapping next to `pinned` with >= GAP unmapped bytes between."""
+    for k in range(1, 64):
+        off = SIZE + GAP * k
+        addr = pinned + off if above else pinned - off
+        addr &= ~(mmap.PAGESIZE - 1)
+        if addr <= 0:
+            continue
+        p = _map_at(addr, SIZE)
+        if p is not None:
+            return p
+    pytest.skip("no free address range next to the pinned buffer")
+
+
+def _fill(ptr, seed):
+    a = np.ctypeslib.as_array((ctypes.c_uint8 * SIZE).from_address(ptr))
+    a[:] = np.random.default_rng(seed).integers(0, 256, size=SIZE, dtype=np.uint8)
+    return a
+
+
+@pytest.fixture
+def pinned():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert qsmd5.lib().qsmd5_init(0) == 0
+    p = qsmd5.alloc_pinned(SIZE)
+    _fill(p, 1)
+    yield p
+    qsmd5.free_pinned(p)
+
+
+def _pairs(lo, hi, L, count=3, off=1000):
+    """count equal-length chunks in each of two buffers, interleaved lo, hi, lo, ...
+    The runtime sorts host lanes by length then index, so lane order keeps
+    this interleaving and every neighbouring pair crosses the allocations."""
+    out = []
+    for i in range(count):
+        out.append((lo + off + i * 3 * L, L))
+        out.append((hi + off + i * 3 * L, L))
+    return out
+
+
+def _check(chunks, flags=0, column=None):
+    if column is None:
+        os.environ.pop("QSMD5_COLUMN_BYTES", None)
+    else:
+        os.environ["QSMD5_COLUMN_BYTES"] = str(column)
+    try:
+        got = qsmd5.hash_batch(chunks, flags=flags)
+    finally:
+        os.environ.pop("QSMD5_COLUMN_BYTES", None)
+    assert got == md5_many(chunks)
+
+
+@pytest.mark.parametrize("above", [True, False], ids=["pageable_above", "pageable_below"])
+@pytest.mark.parametrize("flags", [0, qsmd5.FLAG_HOST], ids=["classified", "flag_host"])
+def test_pinned_and_pageable_equal_lengths(pinned, above, flags):
+    pg = _pageable_near(pinned, above)
+    try:
+        _fill(pg, 2)
+        lo, hi = (pinned, pg) if above else (pg, pinned)
+        for L in LENGTHS:
+            chunks = [(lo + 1000, L), (hi + 1000, L)]  # the seed-0 pair
+            _check(chunks, flags)
+            _check(_pairs(lo, hi, L), flags)
+            # column-staged: every column of the pair is a cross-allocation run
+            _check(_pairs(lo, hi, L), flags, column=1024)
+    finally:
+        _libc.munmap(pg, SIZE)
+
+
+def test_two_pinned_pools(pinned):
+    other = qsmd5.alloc_pinned(SIZE)
+    try:
+        _fill(other, 3)
+        lo, hi = sorted([pinned, other])
+        for L in LENGTHS:
+            _check(_pairs(lo, hi, L))
+            _check(_pairs(lo, hi, L), qsmd5.FLAG_HOST, column=4160)
+    finally:
+        qsmd5.free_pinned(other)
+
+
+def test_two_pageable_mappings_with_a_gap(pinned):
+    """Two pageable mappings with an unmapped hole between them, carved out of
+    one reservation so the layout does not depend on the address space."""
+    span = 2 * SIZE + GAP
+    res = _libc.mmap(None, span, mmap.PROT_NONE, mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS, -1, 0)
+    assert res not in (None, MAP_FAILED)
+    a, b = res, res + SIZE + GAP
+    try:
+        assert _libc.munmap(res + SIZE, GAP) == 0  # the hole
+        for p in (a, b):
+            assert _libc.mprotect(p, SIZE, mmap.PROT_READ | mmap.PROT_WRITE) == 0
+        _fill(a, 4)
+        _fill(b, 5)
+        for L in LENGTHS:
+            _check(_pairs(a, b, L))
+            _check(_pairs(a, b, L), qsmd5.FLAG_HOST, column=1024)
+    finally:
+        _libc.munmap(a, SIZE)
+        _libc.munmap(b, SIZE)
+
+
+def test_file_parts_in_one_buffer_still_one_run(pinned):
+    """The fast path stays: a file's equal parts in one pinned buffer (a single
+    allocation) still go as 2-D runs and hash correctly, whole and in columns."""
+    L = (1 << 20) + 64
+    chunks = [(pinned + i * L, L) for i in range(SIZE // L)]
+    _check(chunks)
+    _check(chunks, column=256 << 10)
