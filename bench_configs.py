@@ -32,6 +32,8 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+# These lines measure the gfx950 kernels: no size routing to the CPU MD5.
+os.environ.setdefault("QSMD5_BACKEND", "gpu")
 sys.path.insert(0, os.path.join(ROOT, "qsfs-fuse_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 MiB = 1 << 20

@@ -140,7 +140,8 @@ def test_two_pageable_mappings_with_a_gap(pinned):
     """Two pageable mappings with an unmapped hole between them, carved out of
     one reservation so the layout does not depend on the address space."""
     span = 2 * SIZE + GAP
-    res = _libc.mmap(None, span, mmap.PROT_NONE, mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS, -1, 0)
+    res = _libc.mmap(None, span, 0,  # PROT_NONE
+                     mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS, -1, 0)
     assert res not in (None, MAP_FAILED)
     a, b = res, res + SIZE + GAP
     try:
