@@ -209,19 +209,26 @@ inline std::vector<CopyRun> plan_copy_runs(size_t n, Src&& src, Width&& w, SpanO
   return runs;
 }
 
-// Multi-GPU split of host chunks (qsmd5_runtime.cpp run_sharded): the chunks
-// (in caller order, lengths host_len) go in contiguous, byte-balanced ranges to
-// k = min(ndev, ceil(total / shard_bytes)) GPUs; a small batch stays on one
-// GPU (a chain costs the same on any number of GPUs; only the host link time
-// shrinks with more).  Returns the shard index of each chunk (0 .. k-1), and
-// k in *nshards.
+// Multi-GPU split of host chunks (qsmd5_runtime.cpp run_sharded).  North star:
+// shard "only when one file's part count exceeds a single GPU's batch"; and
+// host data is bound by each GPU's own PCIe link, so large host batches gain
+// from more links.  The chunks (in caller order, lengths host_len) go in
+// contiguous, byte-balanced ranges to
+//   k = min(ndev, max(ceil(total / shard_bytes), ceil(n / resident)))
+// GPUs: `resident` is the most chains one GPU keeps resident in one launch
+// (32 768, the 64 KiB-ring latency kernel), and shard_bytes the host bytes
+// worth one more link (4 GiB: ~80 ms of PCIe, one 10 MiB chain's time).  A
+// small batch stays on one GPU: a chain costs ~85 ms per 10 MiB on any number
+// of GPUs.  Returns the shard index of each chunk (0 .. k-1), and k in *nshards.
 inline std::vector<uint32_t> plan_shards(const std::vector<uint64_t>& host_len, size_t ndev,
-                                         uint64_t shard_bytes, size_t* nshards) {
+                                         uint64_t shard_bytes, size_t* nshards,
+                                         size_t resident = 32768) {
   uint64_t total = 0;
   for (uint64_t L : host_len) total += L;
   const uint64_t per = std::max<uint64_t>(1, shard_bytes);
-  const size_t k = (size_t)std::min<uint64_t>(std::max<size_t>(1, ndev),
-                                              std::max<uint64_t>(1, (total + per - 1) / per));
+  const uint64_t by_parts = (host_len.size() + std::max<size_t>(1, resident) - 1) / std::max<size_t>(1, resident);
+  const size_t k = (size_t)std::min<uint64_t>(
+      std::max<size_t>(1, ndev), std::max<uint64_t>({1, (total + per - 1) / per, by_parts}));
   std::vector<uint32_t> shard(host_len.size(), 0);
   uint64_t cum = 0;
   size_t sh = 0;

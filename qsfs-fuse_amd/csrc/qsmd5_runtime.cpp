@@ -786,7 +786,7 @@ int run_sharded(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
     host_len[j] = L;
   }
   size_t k = 1;
-  const std::vector<uint32_t> shard = qsmd5::plan_shards(host_len, nd, R.shard_bytes, &k);
+  const std::vector<uint32_t> shard = qsmd5::plan_shards(host_len, nd, R.shard_bytes, &k, qsmd5::kLatency2KernelResident);
   for (size_t j = 0; j < host.size(); ++j) part[shard[j]].push_back(host[j]);
   if (env_u64("QSMD5_TRACE", 0)) {
     for (size_t d = 0; d < nd; ++d)

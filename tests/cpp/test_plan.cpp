@@ -15,8 +15,8 @@
 //      kColMaxPerChunk (+1) columns per chunk;
 //   6. number the segment descriptors of multi-column groups densely (nseg);
 // and the multi-GPU split (plan_shards) must give contiguous shards, on
-// k = min(#GPUs, ceil(bytes / shard_bytes)) GPUs, each within one chunk of an
-// equal share of the bytes.
+// k = min(#GPUs, max(ceil(bytes / shard_bytes), ceil(parts / resident))) GPUs,
+// each within one chunk of an equal share of the bytes.
 // Prints "plan ok <cases>" and exits 0, or the first violation and exits 1.
 #include <stdio.h>
 #include <stdlib.h>
@@ -123,13 +123,15 @@ static void check(const std::vector<uint64_t>& len, uint64_t cap, uint64_t slice
 }
 
 static void check_shards(const std::vector<uint64_t>& len, size_t ndev, uint64_t per,
-                         const char* what) {
+                         const char* what, size_t resident = 32768) {
   size_t k = 0;
-  const std::vector<uint32_t> sh = plan_shards(len, ndev, per, &k);
+  const std::vector<uint32_t> sh = plan_shards(len, ndev, per, &k, resident);
   uint64_t total = 0, longest = 0;
   for (uint64_t L : len) total += L, longest = std::max(longest, L);
-  const size_t want_k = (size_t)std::min<uint64_t>(std::max<size_t>(1, ndev),
-                                                   std::max<uint64_t>(1, (total + per - 1) / per));
+  // more GPUs for more bytes (links) or more parts than one GPU keeps resident
+  const uint64_t by_parts = (len.size() + resident - 1) / resident;
+  const size_t want_k = (size_t)std::min<uint64_t>(
+      std::max<size_t>(1, ndev), std::max<uint64_t>({1, (total + per - 1) / per, by_parts}));
   CHECK(k == want_k, "%s: %zu shards, want %zu", what, k, want_k);
   CHECK(sh.size() == len.size(), "%s: shard list size", what);
   std::vector<uint64_t> bytes(k, 0);
@@ -340,11 +342,13 @@ int main() {
     std::vector<uint64_t> mix;
     for (int i = 0; i < 5000; ++i) mix.push_back(1 + rng() % (64 * MiB));
     sets.push_back(mix);
+    sets.push_back(std::vector<uint64_t>(100000, 1024));  // many small objects: 98 MiB, 100 K parts
     for (const auto& v : sets)
       for (size_t nd : {(size_t)1, (size_t)2, (size_t)3, (size_t)8})
         for (uint64_t per : {(uint64_t)1, 1 * GiB, 4 * GiB, 64 * GiB}) {
           check_shards(v, nd, per, "shards");
-          ++cases;
+          check_shards(v, nd, per, "shards by part count", 1000);
+          cases += 2;
         }
   }
   cases += run_copy_run_cases(rng);

@@ -1,0 +1,28 @@
+"""Runs tests/cpp/multipart_harness (the DoMultiPartUpload flow with the batch
+pre-hash) and returns its JSON report."""
+import json
+import os
+import subprocess
+
+from conftest import ROOT
+
+HARNESS = os.path.join(ROOT, "tests", "cpp", "multipart_harness")
+
+
+def build():
+    src = os.path.join(ROOT, "tests", "cpp", "multipart_harness.cpp")
+    if not os.path.exists(HARNESS) or os.path.getmtime(HARNESS) < os.path.getmtime(src):
+        subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", src,
+                               "-I" + os.path.join(ROOT, "include"),
+                               "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
+                               "-Wl,-rpath,$ORIGIN/../../qsfs-fuse_amd/lib", "-o", HARNESS])
+
+
+def run(args, backend, timeout=300, extra_env=None):
+    build()
+    env = dict(os.environ, QSMD5_BACKEND=backend)
+    env.update(extra_env or {})
+    out = subprocess.run([HARNESS] + list(args), env=env, capture_output=True, text=True,
+                         timeout=timeout)
+    assert out.returncode == 0, out.stderr[-3000:]
+    return json.loads(out.stdout)

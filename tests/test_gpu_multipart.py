@@ -1,0 +1,55 @@
+"""The DoMultiPartUpload flow with the batch pre-hash on the MI355X
+(QSTransferManager.cpp:602-673).
+
+tests/cpp/multipart_harness builds a file held in many separately allocated
+pages, slices it as PrepareUpload does, gathers each wave of parts into pool
+buffers (File::ReadNoLoad, File.cpp:308-375), hashes the wave with ONE
+qsmd5_hash_batch_ex(QSMD5_FLAG_HOST) through qsfs-fuse_amd/host/qsfs_multipart.hpp
+and hands each part's hex digest on.  Every digest is checked against the
+reference-produced golden table.
+"""
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN
+from multipart_util import run
+
+torch = pytest.importorskip("torch")
+MiB = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def gold():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pinned", [False, True], ids=["pageable_pool", "pinned_pool"])
+def test_whole_file_wave_on_the_gpu(gold, pinned):
+    """A pool as large as the file: one wave, one GPU batch of 256 parts."""
+    args = ["--aligned", "--size=%d" % (256 * 10 * MiB), "--pool=256"] + (["--pinned"] if pinned else [])
+    r = run(args, "gpu")
+    assert r["parts"] == 256 and r["waves"] == 1 and r["gpu_waves"] == 1
+    assert r["md5"] == gold[:256]
+    print("256 x 10 MiB paged file, %s pool: gather %.3f s, hash %.3f s (%.1f GiB/s)"
+          % ("pinned" if pinned else "pageable", r["gather_s"], r["hash_s"],
+             2.5 / r["hash_s"]))
+
+
+@pytest.mark.gpu
+@pytest.mark.cpu_backend
+def test_default_pool_routes_waves_by_size(gold):
+    """auto: qsfs's default pool (5 x 10 MiB buffers, 50 MiB heap) gives waves
+    below the GPU break-even, hashed on the CPU; a 64-buffer pool's waves go to
+    the gfx950 kernels.  Same golden digests either way."""
+    small = run(["--aligned", "--size=%d" % (64 * 10 * MiB), "--pool=5"], "auto")
+    assert small["waves"] == 13 and small["cpu_waves"] == 13 and small["gpu_waves"] == 0
+    big = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=64"], "auto")
+    assert big["waves"] == 2 and big["gpu_waves"] == 2
+    assert small["md5"] == gold[:64] and big["md5"] == gold[:128]
+    print("64 parts, pool 5 (CPU waves): hash %.3f s; 128 parts, pool 64 (GPU waves): hash %.3f s"
+          % (small["hash_s"], big["hash_s"]))

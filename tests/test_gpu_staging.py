@@ -55,7 +55,8 @@ def _map_at(addr, size):
 
 def _pageable_near(pinned, above):
     """A pageable mapping next to `pinned` with >= GAP unmapped bytes between."""
-    for k in range(1, 64):
+    # HIP packs its own mappings around pinned buffers: search up to ~16 GiB away
+    for k in list(range(1, 512)) + [512 * j for j in range(2, 16)]:
         off = SIZE + GAP * k
         addr = pinned + off if above else pinned - off
         addr &= ~(mmap.PAGESIZE - 1)
