@@ -478,10 +478,13 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   // neighbouring buffers, which spread evenly over the HBM channels, whatever
   // order a buffer pool handed them out in (512 x 10 MiB pool buffers in
   // shuffled order: 50.8 -> 59.3 GiB/s, profiles/r01_config_pool.jsonl).
-  // Host chunks are staged in lane order into our own skewed layout.
+  // Host chunks are staged in lane order into our own skewed layout; equal
+  // lengths go by address too, so a pool's buffers handed out in any order
+  // (and glibc's downward-growing mmaps, which the kernel merges into one VMA)
+  // line up as ascending constant-stride rows: one 2-D copy per column where
+  // they share a mapping (qsmd5_plan.h plan_copy_runs).
   std::vector<uint32_t> dev_idx, host_idx;
   for (size_t i = 0; i < n; ++i) (kind[i] == kDeviceMem ? dev_idx : host_idx).push_back((uint32_t)i);
-  auto by_len = [&](uint32_t a, uint32_t b) { return len[a] > len[b] || (len[a] == len[b] && a < b); };
   auto by_len_addr = [&](uint32_t a, uint32_t b) {
     if (len[a] != len[b]) return len[a] > len[b];
     const uintptr_t pa = reinterpret_cast<uintptr_t>(chunks[a].ptr);
@@ -492,8 +495,8 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   // chunks: 7.7 ms to sort, ~1 ms to check)
   if (!std::is_sorted(dev_idx.begin(), dev_idx.end(), by_len_addr))
     std::sort(dev_idx.begin(), dev_idx.end(), by_len_addr);
-  if (!std::is_sorted(host_idx.begin(), host_idx.end(), by_len))
-    std::sort(host_idx.begin(), host_idx.end(), by_len);
+  if (!std::is_sorted(host_idx.begin(), host_idx.end(), by_len_addr))
+    std::sort(host_idx.begin(), host_idx.end(), by_len_addr);
 
   const auto t_sorted = std::chrono::steady_clock::now();
   // Staging plan for the host chunks (qsmd5_plan.h; its invariants are tested

@@ -40,6 +40,42 @@ struct PoolBuffer {
   size_t size;
 };
 
+// A transfer-buffer pool carved from ONE allocation (pageable, or pinned
+// through qsmd5_alloc_pinned).  The reference allocates each pool buffer on
+// its own (TransferManager.cpp:103-108); buffers in one allocation at a
+// constant stride let the library move a wave's columns to the GPU as one 2-D
+// copy each instead of one copy per buffer (qsmd5_plan.h plan_copy_runs).
+class BufferSlab {
+ public:
+  BufferSlab(size_t count, size_t size, bool pinned) : count_(count), size_(size), pinned_(pinned) {
+    const size_t bytes = count * size;
+    if (pinned_) {
+      void* p = nullptr;
+      detail::check(qsmd5_alloc_pinned(bytes ? bytes : 1, &p), "qsmd5_alloc_pinned");
+      base_ = static_cast<char*>(p);
+    } else {
+      heap_.resize(bytes ? bytes : 1);
+      base_ = heap_.data();
+    }
+  }
+  ~BufferSlab() {
+    if (pinned_) qsmd5_free_pinned(base_);
+  }
+  BufferSlab(const BufferSlab&) = delete;
+  BufferSlab& operator=(const BufferSlab&) = delete;
+  std::vector<PoolBuffer> buffers() const {
+    std::vector<PoolBuffer> v;
+    for (size_t k = 0; k < count_; ++k) v.push_back(PoolBuffer{base_ + k * size_, size_});
+    return v;
+  }
+
+ private:
+  size_t count_, size_;
+  bool pinned_;
+  char* base_ = nullptr;
+  std::vector<char> heap_;
+};
+
 // What one wave did: parts hashed, and which backend the library picked.
 struct WaveStats {
   size_t waves = 0, parts = 0;

@@ -73,7 +73,7 @@ struct PagedFile {
 int main(int argc, char** argv) {
   uint64_t size = 64ull * 10 * 1024 * 1024;
   size_t pool_n = 5;
-  bool aligned = false, pinned = false;
+  bool aligned = false, pinned = false, slab = false;
   uint32_t seed = 12345;
   uint64_t buf = 10ull << 20;
   for (int i = 1; i < argc; ++i) {
@@ -85,6 +85,7 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--buf=")) buf = strtoull(v, nullptr, 0);
     else if (a == "--aligned") aligned = true;
     else if (a == "--pinned") pinned = true;
+    else if (a == "--slab") slab = true;
     else {
       fprintf(stderr, "unknown argument %s\n", argv[i]);
       return 2;
@@ -114,10 +115,22 @@ int main(int argc, char** argv) {
   if (qsmd5_plan_parts(size, buf, 4ull << 20, 20ull << 20, 0, parts.data(), n, &n)) return 1;
   uint64_t largest = 0;
   for (const qsmd5_part& p : parts) largest = std::max(largest, p.size);
-  // The transfer buffer pool.
+  // The transfer buffer pool: one allocation per buffer, as ResourceManager's
+  // vector<char>(bufSize) each (TransferManager.cpp:103-108), or --slab: one
+  // allocation carved into the buffers (qsmd5::BufferSlab).
   std::vector<std::unique_ptr<std::vector<char>>> owned;
   std::vector<qsmd5::PoolBuffer> pool;
-  for (size_t k = 0; k < pool_n; ++k) {
+  std::unique_ptr<qsmd5::BufferSlab> slab_pool;
+  if (slab) {
+    try {
+      slab_pool.reset(new qsmd5::BufferSlab(pool_n, largest, pinned));
+    } catch (const std::exception& e) {
+      fprintf(stderr, "slab: %s\n", e.what());
+      return 1;
+    }
+    pool = slab_pool->buffers();
+  }
+  for (size_t k = 0; k < pool_n && !slab; ++k) {
     if (pinned) {
       void* p = nullptr;
       if (qsmd5_alloc_pinned(largest, &p)) {
@@ -143,12 +156,13 @@ int main(int argc, char** argv) {
     return 1;
   }
   const double total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  if (pinned)
+  if (pinned && !slab)
     for (auto& b : pool) qsmd5_free_pinned(b.data);
   printf("{\"size\": %llu, \"parts\": %zu, \"pages\": %zu, \"pool\": %zu, \"pinned\": %s, "
-         "\"waves\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"seconds\": %.6f, "
+         "\"slab\": %s, \"waves\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"seconds\": %.6f, "
          "\"gather_s\": %.6f, \"hash_s\": %.6f, \"upload_s\": %.6f, \"part_sizes\": [",
-         (unsigned long long)size, n, file.pages.size(), pool_n, pinned ? "true" : "false", st.waves,
+         (unsigned long long)size, n, file.pages.size(), pool_n, pinned ? "true" : "false",
+         slab ? "true" : "false", st.waves,
          st.gpu_waves, st.cpu_waves, total, st.gather_s, st.hash_s, st.upload_s);
   for (size_t i = 0; i < n; ++i) printf("%s%llu", i ? ", " : "", (unsigned long long)parts[i].size);
   printf("], \"md5\": [");

@@ -28,16 +28,20 @@ def gold():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("slab", [False, True], ids=["buffer_each", "one_slab"])
 @pytest.mark.parametrize("pinned", [False, True], ids=["pageable_pool", "pinned_pool"])
-def test_whole_file_wave_on_the_gpu(gold, pinned):
-    """A pool as large as the file: one wave, one GPU batch of 256 parts."""
-    args = ["--aligned", "--size=%d" % (256 * 10 * MiB), "--pool=256"] + (["--pinned"] if pinned else [])
+def test_whole_file_wave_on_the_gpu(gold, pinned, slab):
+    """A pool as large as the file: one wave, one GPU batch of 512 parts, from
+    pool buffers allocated one by one (as ResourceManager does) or carved from
+    one slab (qsmd5::BufferSlab), pageable or pinned."""
+    args = ["--aligned", "--size=%d" % (512 * 10 * MiB), "--pool=512"]
+    args += (["--pinned"] if pinned else []) + (["--slab"] if slab else [])
     r = run(args, "gpu")
-    assert r["parts"] == 256 and r["waves"] == 1 and r["gpu_waves"] == 1
-    assert r["md5"] == gold[:256]
-    print("256 x 10 MiB paged file, %s pool: gather %.3f s, hash %.3f s (%.1f GiB/s)"
-          % ("pinned" if pinned else "pageable", r["gather_s"], r["hash_s"],
-             2.5 / r["hash_s"]))
+    assert r["parts"] == 512 and r["waves"] == 1 and r["gpu_waves"] == 1
+    assert r["md5"] == gold[:512]
+    print("512 x 10 MiB paged file, %s pool, %s: gather %.3f s, hash %.3f s (%.1f GiB/s)"
+          % ("pinned" if pinned else "pageable", "one slab" if slab else "buffer each",
+             r["gather_s"], r["hash_s"], 5.0 / r["hash_s"]))
 
 
 @pytest.mark.gpu

@@ -27,7 +27,7 @@ from oracle_util import md5_many
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-SIZE = 8 << 20
+SIZE = 32 << 20
 GAP = 2 << 20
 LENGTHS = [55, 88, 4095, 4096, (256 << 10) + 7, 1 << 20]
 
@@ -85,15 +85,17 @@ def pinned():
     qsmd5.free_pinned(p)
 
 
-def _pairs(lo, hi, L, count=3, off=1000):
-    """count equal-length chunks in each of two buffers, interleaved lo, hi, lo, ...
-    The runtime sorts host lanes by length then index, so lane order keeps
-    this interleaving and every neighbouring pair crosses the allocations."""
-    out = []
-    for i in range(count):
-        out.append((lo + off + i * 3 * L, L))
-        out.append((hi + off + i * 3 * L, L))
-    return out
+def _pairs(lo, hi, L, off=1000):
+    """Equal-length chunks whose lane order (by length, then address) has a
+    constant stride that runs from the `lo` allocation across the unmapped gap
+    into `hi`: rows at lo+off + k*D, D = (hi - lo) / 2, k = 0..3 (rows 0-1 in
+    lo, rows 2-3 in hi).  A 2-D copy of all four rows would read the gap; the
+    runtime must cut the run where `lo` ends.  Falls back to the two-row pair
+    when the allocations are too far apart for the progression."""
+    D = (hi - lo) // 2
+    if off + D + L <= SIZE and (hi - lo) % 2 == 0:
+        return [(lo + off + k * D, L) for k in range(4)]
+    return [(lo + off, L), (hi + off, L)]
 
 
 def _check(chunks, flags=0, column=None):
@@ -139,7 +141,8 @@ def test_two_pinned_pools(pinned):
 
 def test_two_pageable_mappings_with_a_gap(pinned):
     """Two pageable mappings with an unmapped hole between them, carved out of
-    one reservation so the layout does not depend on the address space."""
+    one reservation so the layout does not depend on the address space (the
+    four-row progression of _pairs always fits here)."""
     span = 2 * SIZE + GAP
     res = _libc.mmap(None, span, 0,  # PROT_NONE
                      mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS, -1, 0)
