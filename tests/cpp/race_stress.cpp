@@ -21,6 +21,7 @@
 // still reports a race in instrumented code.
 #include <stdint.h>
 #include <stdio.h>
+#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -174,5 +175,15 @@ int main(int argc, char** argv) {
   for (auto& x : th) x.join();
   printf("race_stress %s: %d threads x %d rounds, %ld digests checked, %d failures\n",
          g_bad.load() ? "FAILED" : "ok", T, R, g_checked.load(), g_bad.load());
-  return g_bad.load() ? 1 : 0;
+  fflush(stdout);
+  fflush(stderr);
+  // Leave without running static destructors: the test covers the runtime
+  // while callers race.  The uninstrumented HIP/HSA runtimes' own teardown
+  // (__cxa_finalize of libamdhip64) frees memory that ROCm's ASan device
+  // allocator has already let go of, and its CHECK then fails the process on
+  // some boxes (profiles/r02_gpu_suite_asan_teardown.log) -- after every
+  // digest was checked, inside libhsa-runtime64 frames only.  The planted-race
+  // control returns normally: TSan sets its exit code in its own exit hook.
+  if (g_racy) return g_bad.load() ? 1 : 0;
+  _exit(g_bad.load() ? 1 : 0);
 }
