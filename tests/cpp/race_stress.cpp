@@ -182,8 +182,13 @@ int main(int argc, char** argv) {
   // (__cxa_finalize of libamdhip64) frees memory that ROCm's ASan device
   // allocator has already let go of, and its CHECK then fails the process on
   // some boxes (profiles/r02_gpu_suite_asan_teardown.log) -- after every
-  // digest was checked, inside libhsa-runtime64 frames only.  The planted-race
-  // control returns normally: TSan sets its exit code in its own exit hook.
-  if (g_racy) return g_bad.load() ? 1 : 0;
+  // digest was checked, inside libhsa-runtime64 frames only.  Only the ASan
+  // build leaves early: under TSan the normal exit joins the runtimes' threads
+  // (an _exit would report them as leaked) and runs TSan's exit-code hook.
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
   _exit(g_bad.load() ? 1 : 0);
+#endif
+#endif
+  return g_bad.load() ? 1 : 0;
 }
