@@ -135,15 +135,13 @@ typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 
 // 16-byte load from a 4-byte-aligned global address (global_load_dwordx4;
 // the generic-pointer form would lower to flat_load and force vmcnt(0)+lgkmcnt(0)).
-#ifndef QS_LOAD_NT
-#define QS_LOAD_NT 0
-#endif
+// kNT: the non-temporal cache policy (nt), for message bytes read exactly once.
+template <bool kNT = false>
 __device__ __forceinline__ u32x4 load16_a4(const uint32_t* p) {
-#if QS_LOAD_NT
-  return __builtin_nontemporal_load((const QS_GLOBAL u32x4_a4*)(reinterpret_cast<uintptr_t>(p)));
-#else
-  return *(const QS_GLOBAL u32x4_a4*)(reinterpret_cast<uintptr_t>(p));
-#endif
+  if constexpr (kNT)
+    return __builtin_nontemporal_load((const QS_GLOBAL u32x4_a4*)(reinterpret_cast<uintptr_t>(p)));
+  else
+    return *(const QS_GLOBAL u32x4_a4*)(reinterpret_cast<uintptr_t>(p));
 }
 __device__ __forceinline__ uint32_t load4(const uint32_t* p) {
   return *(const QS_GLOBAL uint32_t*)(reinterpret_cast<uintptr_t>(p));

@@ -200,13 +200,14 @@ struct PcBlockRegs {
   uint32_t e;
 };
 
+template <bool kNT>
 __device__ __forceinline__ void pc_load_block(PcBlockRegs& r, const uint32_t* base, uint32_t off,
                                               uint32_t blk) {
   const uint32_t* q = base + (uint64_t)blk * 16u;
-  r.q[0] = load16_a4(q);
-  r.q[1] = load16_a4(q + 4);
-  r.q[2] = load16_a4(q + 8);
-  r.q[3] = load16_a4(q + 12);
+  r.q[0] = load16_a4<kNT>(q);
+  r.q[1] = load16_a4<kNT>(q + 4);
+  r.q[2] = load16_a4<kNT>(q + 8);
+  r.q[3] = load16_a4<kNT>(q + 12);
   r.e = off ? load4(q + 16) : 0u;  // 17th dword holds message bytes only if off != 0
 }
 
@@ -381,7 +382,10 @@ extern "C" __global__ __launch_bounds__(256) void qsmd5_lcg_fill_kernel(
 // 48.6 -> 54.7 (profiles/r01_ubench_skew.log).  Cost: 63 x skew blocks per
 // wave (0.05% of a 32 MiB chain); shorter chunks never pay it.  0 = off.
 constexpr uint32_t kSkewMinBlocks = 1u << 19;
-template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf>
+//
+// kNT: the producer's loads carry the non-temporal cache policy (chosen per
+// launch by the host, qsmd5_runtime.cpp load_nt_for).
+template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
                                         uint32_t* __restrict__ digests, uint64_t col_off,
@@ -431,7 +435,7 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
 #pragma unroll
         for (int h = 0; h < kHalf; ++h) {
           const uint32_t j = p * kHalf + h;  // virtual block; the lane's block is j - delta
-          pc_load_block(rs[h], base, off, j < delta ? 0u : min(j - delta, last));
+          pc_load_block<kNT>(rs[h], base, off, j < delta ? 0u : min(j - delta, last));
         }
       }
     };
@@ -512,6 +516,19 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc2_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
     uint32_t* __restrict__ digests, uint32_t skew) {
   pc_body<false, 1, 2>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
+}
+
+// The same two kernels with non-temporal producer loads.
+extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_nt_kernel(
+    const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
+    uint32_t* __restrict__ digests, uint32_t skew) {
+  pc_body<false, 1, kPcHalf, true>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
+}
+
+extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc2_nt_kernel(
+    const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
+    uint32_t* __restrict__ digests, uint32_t skew) {
+  pc_body<false, 1, 2, true>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
 }
 
 extern "C" __global__ __launch_bounds__(128) void qsmd5_column_pc_kernel(
@@ -735,16 +752,16 @@ extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_coal_kernel(
 namespace qsmd5 {
 
 hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
-                        int kind, hipStream_t s, uint32_t skew_blocks) {
+                        int kind, hipStream_t s, uint32_t skew_blocks, bool load_nt) {
   if (n == 0) return hipSuccess;
   const uint32_t groups = (n + 63u) / 64u;
   if (kind == kKernelLatency) {
-    hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(groups), dim3(128), 0, s,
-                       static_cast<const ChunkDesc*>(chunks), order, n, digests,
+    hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc_nt_kernel : qsmd5_batch_pc_kernel, dim3(groups),
+                       dim3(128), 0, s, static_cast<const ChunkDesc*>(chunks), order, n, digests,
                        skew_blocks / kPcHalf * kPcHalf);
   } else if (kind == kKernelLatency2) {
-    hipLaunchKernelGGL(qsmd5_batch_pc2_kernel, dim3(groups), dim3(128), 0, s,
-                       static_cast<const ChunkDesc*>(chunks), order, n, digests,
+    hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc2_nt_kernel : qsmd5_batch_pc2_kernel, dim3(groups),
+                       dim3(128), 0, s, static_cast<const ChunkDesc*>(chunks), order, n, digests,
                        skew_blocks / kPcHalf * kPcHalf);
   } else if (kind == kKernelCoalesced) {
     hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3(groups), dim3(64), 0, s,

@@ -27,8 +27,11 @@ constexpr uint32_t kLatency2KernelResident = 2u * 256u * 64u;
 constexpr uint32_t kPcSkewBlocks = 4;
 
 // skew_blocks: latency kernel only (rounded down to a multiple of 4; 0 = off).
+// load_nt: latency kernels only: the producer's loads use the non-temporal
+// cache policy.
 hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
-                        int kind, hipStream_t s, uint32_t skew_blocks = kPcSkewBlocks);
+                        int kind, hipStream_t s, uint32_t skew_blocks = kPcSkewBlocks,
+                        bool load_nt = false);
 // Column-pipelined latency kernel: lane t hashes segment segs[t] = {staged
 // start of bytes [col_off, col_off + col_w) of chunk order[t], that chunk's
 // total length}; state parks in states[4 * order[t]] between columns and the

@@ -444,6 +444,15 @@ int kernel_choice(size_t n, bool aligned16) {
   return aligned16 ? kKernelCoalesced : kKernelThroughput;
 }
 
+// Cache policy of the latency kernels' producer loads for a device batch whose
+// longest chunk is `longest` bytes: QSMD5_LOAD_NT=1 / 0 forces nt / default.
+bool load_nt_for(uint64_t longest) {
+  const char* e = getenv("QSMD5_LOAD_NT");
+  if (e && *e) return strcmp(e, "0") != 0;
+  (void)longest;
+  return false;
+}
+
 using qsmd5::kNoColumns;
 using qsmd5::stage_bytes;
 
@@ -610,10 +619,12 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     }
     return 0;
   };
-  auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt, bool aligned16) -> int {
+  auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt, bool aligned16,
+                    uint64_t longest) -> int {
     if (int rc = mark_first(s)) return rc;
     hipError_t e = qsmd5::launch_batch(d_desc, ord, (uint32_t)cnt, d_dig,
-                                       kernel_choice(cnt, aligned16), s);
+                                       kernel_choice(cnt, aligned16), s, qsmd5::kPcSkewBlocks,
+                                       load_nt_for(longest));
     if (e != hipSuccess) return hip_fail(e, "qsmd5 kernel launch");
     return 0;
   };
@@ -623,7 +634,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     bool aligned16 = true;
     for (uint32_t ci : dev_idx)
       aligned16 = aligned16 && (reinterpret_cast<uintptr_t>(hd[ci].ptr) & 15u) == 0;
-    if (int rc = launch(s0, d_order, dev_idx.size(), aligned16)) return drain(rc);
+    if (int rc = launch(s0, d_order, dev_idx.size(), aligned16, len[dev_idx[0]])) return drain(rc);
   }
   // Host-resident slices: H2D on a copy stream into the slice's ring region
   // (after the kernel that last used the region), then a launch on its group's
@@ -699,7 +710,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       if (e != hipSuccess) return drain(hip_fail(e, "qsmd5 column kernel launch"));
     } else {
       // staged chunks sit at 256-B-aligned offsets plus a 16-B-multiple skew
-      if (int rc = launch(cs, d_order + dev_idx.size() + g.first, sl.active, true))
+      if (int rc = launch(cs, d_order + dev_idx.size() + g.first, sl.active, true, 0))
         return drain(rc);
     }
     if (!one_stream && nregions < slices.size()) {  // a later slice reuses this region

@@ -34,14 +34,16 @@ def test_whole_file_wave_on_the_gpu(gold, pinned, slab):
     """A pool as large as the file: one wave, one GPU batch of 512 parts, from
     pool buffers allocated one by one (as ResourceManager does) or carved from
     one slab (qsmd5::BufferSlab), pageable or pinned."""
-    args = ["--aligned", "--size=%d" % (512 * 10 * MiB), "--pool=512"]
+    args = ["--aligned", "--size=%d" % (512 * 10 * MiB), "--pool=512", "--repeat=3"]
     args += (["--pinned"] if pinned else []) + (["--slab"] if slab else [])
     r = run(args, "gpu")
     assert r["parts"] == 512 and r["waves"] == 1 and r["gpu_waves"] == 1
     assert r["md5"] == gold[:512]
-    print("512 x 10 MiB paged file, %s pool, %s: gather %.3f s, hash %.3f s (%.1f GiB/s)"
+    first, warm = r["hash_s_runs"][0], min(r["hash_s_runs"][1:])
+    print("512 x 10 MiB paged file, %s pool, %s: gather %.3f s; hash first pass %.3f s "
+          "(%.1f GiB/s), reused pool %.3f s (%.1f GiB/s)"
           % ("pinned" if pinned else "pageable", "one slab" if slab else "buffer each",
-             r["gather_s"], r["hash_s"], 5.0 / r["hash_s"]))
+             r["gather_s"], first, 5.0 / first, warm, 5.0 / warm))
 
 
 @pytest.mark.gpu
