@@ -622,8 +622,9 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt, bool aligned16,
                     uint64_t longest) -> int {
     if (int rc = mark_first(s)) return rc;
+    static const uint32_t skew = (uint32_t)env_u64("QSMD5_SKEW_BLOCKS", qsmd5::kPcSkewBlocks);
     hipError_t e = qsmd5::launch_batch(d_desc, ord, (uint32_t)cnt, d_dig,
-                                       kernel_choice(cnt, aligned16), s, qsmd5::kPcSkewBlocks,
+                                       kernel_choice(cnt, aligned16), s, skew,
                                        load_nt_for(longest));
     if (e != hipSuccess) return hip_fail(e, "qsmd5 kernel launch");
     return 0;

@@ -54,7 +54,7 @@ def run(name, part, stride, alloc_bytes=None, separate=False, reps=3):
         host.append(h)
         sample.append((h.ctypes.data, part))
     ok = digs[:8] == md5_many(sample)
-    print(json.dumps({"case": name, "part_MiB": part / MiB, "stride_MiB": stride / MiB,
+    print(json.dumps({"case": name, "tag": os.environ.get("QSMD5_PROBE_TAG", ""), "part_MiB": part / MiB, "stride_MiB": stride / MiB,
                       "alloc_GiB": round((alloc_bytes or ((N - 1) * stride + part)) / GiB, 2)
                       if not separate else "one per part",
                       "GiBps": round(N * part / GiB / best, 3), "ms": round(best * 1e3, 2),
@@ -79,9 +79,25 @@ CASES = {
 }
 
 if __name__ == "__main__":
+    # QSMD5_SKEW_BLOCKS is read once per process: "skew:<blocks>" re-runs the
+    # given cases in a child process with that start skew (0 = off)
+    import subprocess
+    args = sys.argv[1:]
+    if args and args[0].startswith("skew:"):
+        for sk in args[0][5:].split(","):
+            env = dict(os.environ, QSMD5_SKEW_BLOCKS=sk, QSMD5_PROBE_TAG="skew=%s" % sk)
+            r = subprocess.run([sys.executable, __file__] + args[1:], env=env)
+            if r.returncode:
+                sys.exit(r.returncode)
+        sys.exit(0)
     import torch
     import qsmd5
     assert torch.cuda.is_available()
     assert qsmd5.lib().qsmd5_init(0) == 0
-    for c in (sys.argv[1:] or list(CASES)):
-        CASES[c]()
+    for c in (args or list(CASES)):
+        if c in CASES:
+            CASES[c]()
+        else:  # "p<part MiB>+<pad bytes>": parts at a stride of part + pad
+            part, pad = c[1:].split("+")
+            run("%s MiB parts, +%s B stride pad" % (part, pad), int(part) * MiB,
+                int(part) * MiB + int(pad))
