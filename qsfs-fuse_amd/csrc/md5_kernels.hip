@@ -385,21 +385,27 @@ constexpr uint32_t kSkewMinBlocks = 1u << 19;
 //
 // kNT: the producer's loads carry the non-temporal cache policy (chosen per
 // launch by the host, qsmd5_runtime.cpp load_nt_for).
-template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false>
+// kTrace (ubench only): the chain wave's lane 0 stamps s_memtime and
+// s_memrealtime every 4096 phases into trace[workgroup][2 * (p / 4096) + {0,1}].
+template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
                                         uint32_t* __restrict__ digests, uint64_t col_off,
                                         uint64_t col_w, uint32_t* __restrict__ states,
-                                        uint32_t skew) {
+                                        uint32_t skew, uint64_t* __restrict__ trace = nullptr,
+                                        uint32_t lanes = 64) {
   __shared__ u32x4 ring[2 * kHalf][16][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
-  const uint32_t t = blockIdx.x * 64u + lane;
+  // `lanes` chains per workgroup (64, or fewer to spread long chains over more
+  // CUs); lanes past it, or past the batch, idle.
+  const uint32_t t = blockIdx.x * lanes + lane;
+  const bool live = lane < lanes && t < n;
   uint32_t idx = 0;
   ChunkDesc cd = {nullptr, 0};
   uint64_t seg = 0;     // message bytes of this lane's segment
   bool final = true;    // this segment ends the chunk
-  if (t < n) {
+  if (live) {
     if (kColumn) {
       idx = order[t];
       cd = chunks[t];
@@ -475,9 +481,9 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
   // Phases in which every live lane still has all kHalf blocks run without a
   // per-block lane predicate (wave-uniform branch on an SGPR).
   const uint32_t live_lo = rfl_u32((wave_max_u32(delta) + kHalf - 1) / kHalf);
-  const uint32_t live_hi = rfl_u32(wave_min_u32(t < n ? nblk + delta : 0xffffffffu) / kHalf);
+  const uint32_t live_hi = rfl_u32(wave_min_u32(live ? nblk + delta : 0xffffffffu) / kHalf);
   uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
-  if (kColumn && col_off != 0 && t < n) {
+  if (kColumn && col_off != 0 && live) {
     const u32x4 s4 = *reinterpret_cast<const u32x4*>(states + 4u * (uint64_t)idx);
     st[0] = s4.x;
     st[1] = s4.y;
@@ -486,6 +492,13 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
   }
   lds_barrier();
   for (uint32_t p = 0; p < phases; ++p) {
+    if constexpr (kTrace) {
+      if (lane == 0 && (p & 4095u) == 0u) {
+        uint64_t* tr = trace + (uint64_t)blockIdx.x * 1024u + 2u * (p >> 12);
+        tr[0] = __builtin_amdgcn_s_memtime();
+        tr[1] = __builtin_amdgcn_s_memrealtime();
+      }
+    }
     const uint32_t s0 = (p & 1u) * kHalf;
     if (p >= live_lo && p < live_hi)
       chain_phase<true, kHalf>(st, ring, s0, lane, p * kHalf - delta, nblk);
@@ -493,7 +506,7 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
       chain_phase<false, kHalf>(st, ring, s0, lane, p * kHalf - delta, nblk);
     lds_barrier();
   }
-  if (t >= n) return;
+  if (!live) return;
   if (kColumn && !final) {
     u32x4 o = {st[0], st[1], st[2], st[3]};
     *reinterpret_cast<u32x4*>(states + 4u * (uint64_t)idx) = o;
@@ -506,29 +519,29 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
 
 extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
-    uint32_t* __restrict__ digests, uint32_t skew) {
-  pc_body<false>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
+    uint32_t* __restrict__ digests, uint32_t skew, uint32_t lanes) {
+  pc_body<false>(chunks, order, n, digests, 0, ~0ull, nullptr, skew, nullptr, lanes);
 }
 
 // 2-block phases: a 64 KiB ring, so two workgroups (four waves) share a CU and
 // one launch keeps 2 x 256 x 64 chunks resident (kKernelLatency2).
 extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc2_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
-    uint32_t* __restrict__ digests, uint32_t skew) {
-  pc_body<false, 1, 2>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
+    uint32_t* __restrict__ digests, uint32_t skew, uint32_t lanes) {
+  pc_body<false, 1, 2>(chunks, order, n, digests, 0, ~0ull, nullptr, skew, nullptr, lanes);
 }
 
 // The same two kernels with non-temporal producer loads.
 extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_nt_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
-    uint32_t* __restrict__ digests, uint32_t skew) {
-  pc_body<false, 1, kPcHalf, true>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
+    uint32_t* __restrict__ digests, uint32_t skew, uint32_t lanes) {
+  pc_body<false, 1, kPcHalf, true>(chunks, order, n, digests, 0, ~0ull, nullptr, skew, nullptr, lanes);
 }
 
 extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc2_nt_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
-    uint32_t* __restrict__ digests, uint32_t skew) {
-  pc_body<false, 1, 2, true>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
+    uint32_t* __restrict__ digests, uint32_t skew, uint32_t lanes) {
+  pc_body<false, 1, 2, true>(chunks, order, n, digests, 0, ~0ull, nullptr, skew, nullptr, lanes);
 }
 
 extern "C" __global__ __launch_bounds__(128) void qsmd5_column_pc_kernel(
@@ -752,17 +765,19 @@ extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_coal_kernel(
 namespace qsmd5 {
 
 hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
-                        int kind, hipStream_t s, uint32_t skew_blocks, bool load_nt) {
+                        int kind, hipStream_t s, uint32_t skew_blocks, bool load_nt, uint32_t lanes) {
   if (n == 0) return hipSuccess;
   const uint32_t groups = (n + 63u) / 64u;
+  if (lanes < 1 || lanes > 64) return hipErrorInvalidValue;
+  const uint32_t pc_groups = (n + lanes - 1) / lanes;
   if (kind == kKernelLatency) {
-    hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc_nt_kernel : qsmd5_batch_pc_kernel, dim3(groups),
+    hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc_nt_kernel : qsmd5_batch_pc_kernel, dim3(pc_groups),
                        dim3(128), 0, s, static_cast<const ChunkDesc*>(chunks), order, n, digests,
-                       skew_blocks / kPcHalf * kPcHalf);
+                       skew_blocks / kPcHalf * kPcHalf, lanes);
   } else if (kind == kKernelLatency2) {
-    hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc2_nt_kernel : qsmd5_batch_pc2_kernel, dim3(groups),
+    hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc2_nt_kernel : qsmd5_batch_pc2_kernel, dim3(pc_groups),
                        dim3(128), 0, s, static_cast<const ChunkDesc*>(chunks), order, n, digests,
-                       skew_blocks / kPcHalf * kPcHalf);
+                       skew_blocks / kPcHalf * kPcHalf, lanes);
   } else if (kind == kKernelCoalesced) {
     hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3(groups), dim3(64), 0, s,
                        static_cast<const ChunkDesc*>(chunks), order, n, digests);

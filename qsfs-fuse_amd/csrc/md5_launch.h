@@ -29,9 +29,11 @@ constexpr uint32_t kPcSkewBlocks = 4;
 // skew_blocks: latency kernel only (rounded down to a multiple of 4; 0 = off).
 // load_nt: latency kernels only: the producer's loads use the non-temporal
 // cache policy.
+// lanes: latency kernels only: chains per workgroup (1..64; fewer spread long
+// chains over more CUs).
 hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
                         int kind, hipStream_t s, uint32_t skew_blocks = kPcSkewBlocks,
-                        bool load_nt = false);
+                        bool load_nt = false, uint32_t lanes = 64);
 // Column-pipelined latency kernel: lane t hashes segment segs[t] = {staged
 // start of bytes [col_off, col_off + col_w) of chunk order[t], that chunk's
 // total length}; state parks in states[4 * order[t]] between columns and the

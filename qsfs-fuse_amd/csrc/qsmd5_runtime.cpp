@@ -453,6 +453,23 @@ bool load_nt_for(uint64_t longest) {
   return false;
 }
 
+// Chains per workgroup of the latency kernel for a device batch of n chunks
+// whose longest has `longest` bytes.  64 lanes of a wave reading 64 long
+// chunks in lockstep run ~7% slower once the parts reach 64 MiB (and at exact
+// 32 MiB strides): 1293-1300 cycles per block from the first block on, at an
+// unchanged 2.40 GHz, against 1225 for 56 MiB parts
+// (profiles/r02_plateau_lanes.log, ubench ptrace).  Half a wave per CU --
+// half the address span per CU -- brings them back to 1235-1242.  The chains
+// then occupy twice the CUs, so only while one round still holds the batch
+// (256 CUs x 32 lanes).  QSMD5_PC_LANES overrides (1..64).
+uint32_t pc_lanes_for(size_t n, uint64_t longest) {
+  const uint64_t forced = env_u64("QSMD5_PC_LANES", 0);
+  if (forced >= 1 && forced <= 64) return (uint32_t)forced;
+  constexpr uint64_t kLongPart = 32ull << 20;  // the skewed regime (kSkewMinBlocks blocks)
+  if (longest >= kLongPart && n <= qsmd5::kLatencyKernelResident / 2) return 32;
+  return 64;
+}
+
 using qsmd5::kNoColumns;
 using qsmd5::stage_bytes;
 
@@ -625,7 +642,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     static const uint32_t skew = (uint32_t)env_u64("QSMD5_SKEW_BLOCKS", qsmd5::kPcSkewBlocks);
     hipError_t e = qsmd5::launch_batch(d_desc, ord, (uint32_t)cnt, d_dig,
                                        kernel_choice(cnt, aligned16), s, skew,
-                                       load_nt_for(longest));
+                                       load_nt_for(longest), pc_lanes_for(cnt, longest));
     if (e != hipSuccess) return hip_fail(e, "qsmd5 kernel launch");
     return 0;
   };

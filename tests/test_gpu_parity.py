@@ -155,6 +155,37 @@ def test_start_skew_wave_mixed_lengths():
     assert got == want
 
 
+@pytest.mark.parametrize("lanes,nt", [("1", "0"), ("7", "0"), ("32", "1"), ("63", "0")])
+def test_latency_kernel_lanes_and_cache_policy(lanes, nt, monkeypatch):
+    """QSMD5_PC_LANES: chains per workgroup of the latency kernel (the runtime
+    picks 32 for parts >= 32 MiB, pc_lanes_for); QSMD5_LOAD_NT: the producer's
+    cache policy.  Odd lane counts leave the tail lanes of every workgroup and
+    a partial last workgroup idle; every chunk must still hash its own bytes."""
+    monkeypatch.setenv("QSMD5_PC_LANES", lanes)
+    monkeypatch.setenv("QSMD5_LOAD_NT", nt)
+    monkeypatch.setenv("QSMD5_KERNEL", "pc")
+    lens = [0, 1, 55, 64, 65, 4096 + 3, 300001] + [1 + 977 * i for i in range(143)]
+    offs, pos = [], 0
+    for i, L in enumerate(lens):
+        pos += 1 + (i % 5)
+        offs.append(pos)
+        pos += L
+    t = dev_lcg(4711, pos + 64)
+    raw = t.cpu().numpy()
+    want = md5_many([(raw.ctypes.data + o, L) for o, L in zip(offs, lens)])
+    assert qsmd5.hash_batch([(t.data_ptr() + o, L) for o, L in zip(offs, lens)]) == want
+
+
+def test_long_parts_run_at_half_a_wave_per_cu():
+    """Parts >= 32 MiB take the 32-lanes-per-workgroup launch (pc_lanes_for):
+    40 x 33 MiB (+ 3 B) device parts against the oracle."""
+    L, n = 33 * MiB + 3, 40
+    t = dev_lcg(8080, L, nchunks=n, stride=L + 13)
+    raw = t.cpu().numpy()
+    want = md5_many([(raw.ctypes.data + i * (L + 13), L) for i in range(n)])
+    assert qsmd5.hash_batch([(t.data_ptr() + i * (L + 13), L) for i in range(n)]) == want
+
+
 def _device_batch(n, L, seed0):
     t = dev_lcg(seed0, L, nchunks=n)
     desc = torch.empty((n, 2), dtype=torch.int64)

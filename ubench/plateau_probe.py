@@ -21,7 +21,9 @@ MiB, GiB = 1 << 20, 1 << 30
 N = 512
 
 
-def run(name, part, stride, alloc_bytes=None, separate=False, reps=3):
+def run(name, part, stride, alloc_bytes=None, separate=False, reps=3, n=None):
+    global N
+    N = n or 512
     import torch
     import qsmd5
     from oracle_util import md5_many
@@ -54,7 +56,7 @@ def run(name, part, stride, alloc_bytes=None, separate=False, reps=3):
         host.append(h)
         sample.append((h.ctypes.data, part))
     ok = digs[:8] == md5_many(sample)
-    print(json.dumps({"case": name, "tag": os.environ.get("QSMD5_PROBE_TAG", ""), "part_MiB": part / MiB, "stride_MiB": stride / MiB,
+    print(json.dumps({"case": name, "parts": N, "tag": os.environ.get("QSMD5_PROBE_TAG", ""), "part_MiB": part / MiB, "stride_MiB": stride / MiB,
                       "alloc_GiB": round((alloc_bytes or ((N - 1) * stride + part)) / GiB, 2)
                       if not separate else "one per part",
                       "GiBps": round(N * part / GiB / best, 3), "ms": round(best * 1e3, 2),
@@ -97,7 +99,8 @@ if __name__ == "__main__":
     for c in (args or list(CASES)):
         if c in CASES:
             CASES[c]()
-        else:  # "p<part MiB>+<pad bytes>": parts at a stride of part + pad
-            part, pad = c[1:].split("+")
-            run("%s MiB parts, +%s B stride pad" % (part, pad), int(part) * MiB,
-                int(part) * MiB + int(pad))
+        else:  # "p<part MiB>+<pad bytes>[x<parts>]": parts at a stride of part + pad
+            spec, _, nparts = c[1:].partition("x")
+            part, pad = spec.split("+")
+            run("%s x %s MiB parts, +%s B stride pad" % (nparts or 512, part, pad), int(part) * MiB,
+                int(part) * MiB + int(pad), n=int(nparts) if nparts else None)

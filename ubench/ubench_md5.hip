@@ -47,6 +47,14 @@ __global__ __launch_bounds__(128) void k_pc_half2(const ChunkDesc* __restrict__ 
   pc_body<false, 1, 2>(c, o, n, d, 0, ~0ull, nullptr, skew);
 }
 
+// Latency kernel with the chain wave stamping its clocks every 4096 phases.
+__global__ __launch_bounds__(128) void k_pc_trace(const ChunkDesc* __restrict__ c,
+                                                  const uint32_t* __restrict__ o, uint32_t n,
+                                                  uint32_t* __restrict__ d, uint32_t skew,
+                                                  uint64_t* __restrict__ tr, uint32_t lanes) {
+  pc_body<false, 1, kPcHalf, false, true>(c, o, n, d, 0, ~0ull, nullptr, skew, tr, lanes);
+}
+
 // Coalesced kernel with immediate-offset DMA in the fast region.
 __global__ __launch_bounds__(64) void k_coal_imm(const ChunkDesc* __restrict__ c,
                                                  const uint32_t* __restrict__ o, uint32_t n,
@@ -197,14 +205,6 @@ static uint32_t g_skew = kPcSkewBlocks;  // latency kernel start skew (blocks pe
 
 // lane order: 0 chunk i; 1 lane l of wave w gets chunk l * (B/64) + w; 2 random
 // permutation inside each group of 64; 3 random permutation of all chunks
-// lane order: 0 chunk i; 1 lane l of wave w gets chunk l * (B/64) + w; 2 random
-// permutation inside each group of 64; 3 random permutation of all chunks
-template <int kPerm, uint32_t kMin>
-__global__ __launch_bounds__(128) void k_pc_perm(const ChunkDesc* __restrict__ chunks,
-                                                 const uint32_t* __restrict__ order, uint32_t n,
-                                                 uint32_t* __restrict__ digests, uint32_t skew) {
-  pc_body<false, 1, kPcHalf, kPerm, kMin>(chunks, order, n, digests, 0, ~0ull, nullptr, skew);
-}
 static int g_interleave = 0;
 static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint64_t pad = 0) {
   uint64_t stride = ((L + 255) & ~uint64_t(255)) + pad;
@@ -249,7 +249,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
                          (uint32_t)B, d_dig);
     else if (which == 1)
       hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
-                         (uint32_t)B, d_dig, g_skew);
+                         (uint32_t)B, d_dig, g_skew, 64u);
     else if (which == 2)
       hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3(grid), dim3(64), 0, 0, d_desc, nullptr,
                          (uint32_t)B, d_dig);
@@ -354,7 +354,7 @@ static int run_edges(int which) {
                        (uint32_t)n, dg);
   else if (which == 1)
     hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
-                       (uint32_t)n, dg, g_skew);
+                       (uint32_t)n, dg, g_skew, 64u);
   else if (which == 2)
     hipLaunchKernelGGL(qsmd5_batch_coal_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, dd, nullptr,
                        (uint32_t)n, dg);
@@ -848,6 +848,66 @@ int main(int argc, char** argv) {
       run_md5(100, (32ull << 20) + 64 * 7 + 13, 2, true, w, 0);  // ragged tail, partial wave
     }
     return bad ? 1 : 0;
+  }
+  if (!strcmp(mode, "ptrace")) {
+    // ptrace B MiB pad: cycles per 64-B block and the SCLK of the latency
+    // kernel's chain waves, per 16384 blocks (1 MiB) of progress: does a long
+    // chain slow down with its block index, with time, or from the start?
+    const int B = argc > 2 ? atoi(argv[2]) : 512;
+    const uint64_t L = (argc > 3 ? strtoull(argv[3], nullptr, 10) : 64) << 20;
+    const uint64_t pad = argc > 4 ? strtoull(argv[4], nullptr, 10) : 4352;
+    const uint32_t lanes = argc > 5 ? (uint32_t)atoi(argv[5]) : 64u;
+    const uint64_t stride = L + pad;
+    uint8_t* d_data;
+    CK(hipMalloc(&d_data, stride * (uint64_t)B));
+    const uint64_t segs = (L + 1023) / 1024;
+    hipLaunchKernelGGL(qsmd5_lcg_fill_kernel, dim3((segs * B + 255) / 256), dim3(256), 0, 0, d_data,
+                       stride, L, 12345u, (uint32_t)B, segs);
+    std::vector<ChunkDesc> h(B);
+    for (int i = 0; i < B; ++i) h[i] = {d_data + (uint64_t)i * stride, L};
+    ChunkDesc* d_c;
+    uint32_t* d_dig;
+    uint64_t* d_tr;
+    const int groups = (B + (int)lanes - 1) / (int)lanes;
+    CK(hipMalloc(&d_c, sizeof(ChunkDesc) * B));
+    CK(hipMalloc(&d_dig, 16 * B));
+    CK(hipMalloc(&d_tr, 8 * 1024 * groups));
+    CK(hipMemset(d_tr, 0, 8 * 1024 * groups));
+    CK(hipMemcpy(d_c, h.data(), sizeof(ChunkDesc) * B, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(k_pc_trace, dim3(groups), dim3(128), 0, 0, d_c, nullptr, (uint32_t)B, d_dig,
+                       g_skew, d_tr, lanes);
+    CK(hipEventRecord(e1, 0));
+    CK(hipDeviceSynchronize());
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<uint64_t> tr(1024 * groups);
+    CK(hipMemcpy(tr.data(), d_tr, 8 * tr.size(), hipMemcpyDeviceToHost));
+    const uint64_t nblk = L / 64;
+    printf("ptrace B=%d L=%llu MiB pad=%llu skew=%u lanes=%u: %.2f ms, %.1f cycles/block overall at 2.4 GHz\n",
+           B, (unsigned long long)(L >> 20), (unsigned long long)pad, g_skew, lanes, ms,
+           ms * 1e-3 * 2.4e9 / (double)nblk);
+    const int pts = (int)std::min<uint64_t>(512, (nblk / 4 + 4095) / 4096);
+    for (int g = 0; g < groups; g += std::max(1, groups / 4)) {
+      printf("  wg %d: MiB-index:cycles/block@GHz", g);
+      for (int k = 1; k < pts; ++k) {
+        const uint64_t* a = &tr[(uint64_t)g * 1024 + 2 * (k - 1)];
+        const uint64_t* b = &tr[(uint64_t)g * 1024 + 2 * k];
+        if (!b[0] || !a[0]) break;
+        const double cyc = (double)(b[0] - a[0]), real = (double)(b[1] - a[1]);
+        if (k % std::max(1, pts / 16) == 0 || k == pts - 1)
+          printf(" %d:%.0f@%.2f", k, cyc / 16384.0, cyc / real * 0.1);
+      }
+      printf("\n");
+    }
+    CK(hipFree(d_data));
+    CK(hipFree(d_c));
+    CK(hipFree(d_dig));
+    CK(hipFree(d_tr));
+    return 0;
   }
   if (!strcmp(mode, "cross")) {
     // latency (pc) vs coalesced kernel around the selection threshold (16384 chunks)
