@@ -55,6 +55,44 @@ __global__ __launch_bounds__(128) void k_pc_trace(const ChunkDesc* __restrict__ 
   pc_body<false, 1, kPcHalf, false, true>(c, o, n, d, 0, ~0ull, nullptr, skew, tr, lanes);
 }
 
+// Decomposition of the latency kernel's chain-wave cost per 64-B block:
+//   kMode 0: chain_phase<true> over a pre-filled LDS ring, no producer, no barrier
+//   kMode 1: mode 0 + lds_barrier() after every phase, with a second wave that
+//            only meets the barriers (the producer's role without its loads)
+//   kMode 2: md5_compress_mk from registers (no LDS reads at all)
+// out[0] = s_memtime cycles of the chain wave over `phases` phases of 4 blocks.
+template <int kMode>
+__global__ __launch_bounds__(128) void k_chain_cost(uint64_t* out, uint32_t* sink, int phases) {
+  __shared__ u32x4 ring[2 * kPcHalf][16][64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (int k = threadIdx.x; k < 2 * kPcHalf * 16 * 64; k += blockDim.x)
+    (&ring[0][0][0])[k] = u32x4{(uint32_t)k * 2654435761u, (uint32_t)k, 7u, 9u};
+  __syncthreads();
+  if (wave == 1) {
+    if (kMode == 1)
+      for (int p = 0; p < phases; ++p) lds_barrier();
+    return;
+  }
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  uint32_t mk[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) mk[i] = (&ring[0][0][0])[i * 64 + lane].x;
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int p = 0; p < phases; ++p) {
+    if constexpr (kMode == 2) {
+#pragma unroll
+      for (int h = 0; h < kPcHalf; ++h) md5_compress_mk(st, mk);
+      asm volatile("" : "+v"(st[0]), "+v"(st[1]));
+    } else {
+      chain_phase<true>(st, ring, (uint32_t)(p & 1) * kPcHalf, lane, 0, 1u << 30);
+      if (kMode == 1) lds_barrier();
+    }
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[0] = t1 - t0;
+  sink[lane] = st[0] ^ st[1] ^ st[2] ^ st[3];
+}
+
 // Coalesced kernel with immediate-offset DMA in the fast region.
 __global__ __launch_bounds__(64) void k_coal_imm(const ChunkDesc* __restrict__ c,
                                                  const uint32_t* __restrict__ o, uint32_t n,
@@ -907,6 +945,28 @@ int main(int argc, char** argv) {
     CK(hipFree(d_c));
     CK(hipFree(d_dig));
     CK(hipFree(d_tr));
+    return 0;
+  }
+  if (!strcmp(mode, "chaincost")) {
+    // cycles per 64-B block of the chain wave, by what it does besides the steps
+    uint64_t* d_out;
+    uint32_t* d_sink;
+    CK(hipMalloc(&d_out, 8));
+    CK(hipMalloc(&d_sink, 4 * 128));
+    const int phases = 4096;
+    auto one = [&](auto kern, const char* what) {
+      hipLaunchKernelGGL(kern, dim3(1), dim3(128), 0, 0, d_out, d_sink, 16);
+      hipLaunchKernelGGL(kern, dim3(1), dim3(128), 0, 0, d_out, d_sink, phases);
+      CK(hipDeviceSynchronize());
+      uint64_t cyc;
+      CK(hipMemcpy(&cyc, d_out, 8, hipMemcpyDeviceToHost));
+      printf("  %-58s %.1f cycles/block\n", what, (double)cyc / (phases * kPcHalf));
+    };
+    one(k_chain_cost<2>, "steps from registers (no LDS, no barrier)");
+    one(k_chain_cost<0>, "chain_phase: 16 ds_read_b128 + 1 wait per block");
+    one(k_chain_cost<1>, "chain_phase + lds_barrier per 4 blocks (2nd wave barriers only)");
+    CK(hipFree(d_out));
+    CK(hipFree(d_sink));
     return 0;
   }
   if (!strcmp(mode, "cross")) {
