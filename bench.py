@@ -325,16 +325,21 @@ def main():
                      "kernel_ms_avg": round(kavg_ms, 3),
                      "algorithmic_bytes_per_launch": B * L},
         # the stream-parallelism ceiling beside % of HBM peak.  A chunk
-        # is one serial chain; its floor is 4 dependent VALU per MD5 step (bitop3,
-        # add3, alignbit, add) = 256 per 64-B block, each issued every 4.44 cycles
-        # by one wave (measured, profiles/r01_ubench_issue_and_kernels.log), at the
-        # 2.4 GHz the chip holds with 8 CUs busy.
+        # is one serial chain of 64 MD5 steps per 64-B block, each step 4 dependent
+        # VALU (bitop3, add3, alignbit, add).  Measured on gfx950 with one wave alone
+        # on its SIMD (ubench chaincost, profiles/r02_chaincost.log): the steps from
+        # registers take 1045 cycles per block; fed from the LDS ring (16
+        # ds_read_b128 per block) 1155.  The ceiling uses the register floor, at the
+        # 2.4 GHz the chip holds with a few CUs busy.
         "stream_ceiling": {
-            "chains": ntot // world, "floor_cycles_per_block": 256 * 4.44,
-            "GBps": round(B * 64 * 2.4e9 / (256 * 4.44) / 1e9, 2),
-            "frac": round(achieved_gbs / (B * 64 * 2.4e9 / (256 * 4.44) / 1e9), 4),
+            "chains": ntot // world, "floor_cycles_per_block": 1045.0,
+            "lds_fed_floor_cycles_per_block": 1155.0,
+            "GBps": round(B * 64 * 2.4e9 / 1045.0 / 1e9, 2),
+            "frac": round(achieved_gbs / (B * 64 * 2.4e9 / 1045.0 / 1e9), 4),
             "note": "achieved / (B x per-chain issue floor): how close the kernel is to what "
-                    "B serial MD5 chains allow on one GPU"},
+                    "B serial MD5 chains allow on one GPU; the floor has no operand "
+                    "traffic at all, so 1045 / 1155 = 0.905 is the most an LDS-fed chain "
+                    "can reach"},
         "per_chain": {"GiBps": round(B * L / (1 << 30) / (kavg_ms * 1e-3) / B, 4),
                       "cycles_per_64B_block_at_2p4GHz": round(kavg_ms * 1e-3 * 2.4e9 / (L / 64), 1),
                       "note": "MD5 is a serial chain per chunk; at batch=512 the job rate is "

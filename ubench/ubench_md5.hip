@@ -55,13 +55,68 @@ __global__ __launch_bounds__(128) void k_pc_trace(const ChunkDesc* __restrict__ 
   pc_body<false, 1, kPcHalf, false, true>(c, o, n, d, 0, ~0ull, nullptr, skew, tr, lanes);
 }
 
+// chain_phase with the 16 LDS reads of block h+1 spread through block h's 256
+// VALU (one read per kR VALU, placed with sched_group_barrier) instead of
+// issued together at the block's start.
+template <int kR, int kHalf = kPcHalf>
+__device__ __forceinline__ void chain_phase_spread(uint32_t (&st)[4], const u32x4 (*ring)[16][64],
+                                                   uint32_t s0, uint32_t lane) {
+  u32x4 a[16], b[16];
+#pragma unroll
+  for (int g = 0; g < 16; ++g) a[g] = ring[s0][g][lane];
+#pragma unroll
+  for (int h = 0; h < kHalf; ++h) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
+    __builtin_amdgcn_sched_barrier(0);
+    u32x4 (&cur)[16] = (h & 1) ? b : a;
+    u32x4 (&nxt)[16] = (h & 1) ? a : b;
+    if (h + 1 < kHalf) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) nxt[g] = ring[s0 + h + 1][g][lane];
+    }
+    uint32_t mk[64];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      mk[4 * g + 0] = cur[g].x;
+      mk[4 * g + 1] = cur[g].y;
+      mk[4 * g + 2] = cur[g].z;
+      mk[4 * g + 3] = cur[g].w;
+    }
+    md5_compress_mk(st, mk);
+    if (h + 1 < kHalf) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x0100, 1, 0);   // one DS read
+        __builtin_amdgcn_sched_group_barrier(0x0002, kR, 0);  // kR VALU
+      }
+    }
+  }
+}
+
+template <int kR>
+__global__ __launch_bounds__(128) void k_chain_spread(uint64_t* out, uint32_t* sink, int phases) {
+  __shared__ u32x4 ring[2 * kPcHalf][16][64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (int k = threadIdx.x; k < 2 * kPcHalf * 16 * 64; k += blockDim.x)
+    (&ring[0][0][0])[k] = u32x4{(uint32_t)k * 2654435761u, (uint32_t)k, 7u, 9u};
+  __syncthreads();
+  if (wave == 1) return;
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int p = 0; p < phases; ++p) chain_phase_spread<kR>(st, ring, (uint32_t)(p & 1) * kPcHalf, lane);
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[0] = t1 - t0;
+  sink[lane] = st[0] ^ st[1] ^ st[2] ^ st[3];
+}
+
 // Decomposition of the latency kernel's chain-wave cost per 64-B block:
 //   kMode 0: chain_phase<true> over a pre-filled LDS ring, no producer, no barrier
 //   kMode 1: mode 0 + lds_barrier() after every phase, with a second wave that
 //            only meets the barriers (the producer's role without its loads)
 //   kMode 2: md5_compress_mk from registers (no LDS reads at all)
 // out[0] = s_memtime cycles of the chain wave over `phases` phases of 4 blocks.
-template <int kMode>
+template <int kMode, uint32_t kLanes = 64>
 __global__ __launch_bounds__(128) void k_chain_cost(uint64_t* out, uint32_t* sink, int phases) {
   __shared__ u32x4 ring[2 * kPcHalf][16][64];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -73,6 +128,7 @@ __global__ __launch_bounds__(128) void k_chain_cost(uint64_t* out, uint32_t* sin
       for (int p = 0; p < phases; ++p) lds_barrier();
     return;
   }
+  if (lane >= kLanes) return;  // fewer active chains: a narrower EXEC mask
   uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
   uint32_t mk[64];
 #pragma unroll
@@ -965,6 +1021,11 @@ int main(int argc, char** argv) {
     one(k_chain_cost<2>, "steps from registers (no LDS, no barrier)");
     one(k_chain_cost<0>, "chain_phase: 16 ds_read_b128 + 1 wait per block");
     one(k_chain_cost<1>, "chain_phase + lds_barrier per 4 blocks (2nd wave barriers only)");
+    one(k_chain_cost<0, 32>, "chain_phase, 32 active lanes");
+    one(k_chain_cost<0, 16>, "chain_phase, 16 active lanes");
+    one(k_chain_cost<0, 1>, "chain_phase, 1 active lane");
+    one(k_chain_cost<2, 32>, "steps from registers, 32 active lanes");
+    one(k_chain_spread<16>, "reads spread: 1 DS read per 16 VALU");
     CK(hipFree(d_out));
     CK(hipFree(d_sink));
     return 0;
