@@ -759,6 +759,44 @@ extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_coal_kernel(
 #undef QS_LP
 
 // ---------------------------------------------------------------------------
+// Gather of host rows into the staging ring (qsmd5_runtime.cpp run_batch).
+// Rows that cannot share a 2-D DMA copy -- pinned buffers in separate
+// allocations, each one HIP allocation on its own -- would otherwise cost one
+// hipMemcpyAsync each (~8-10 us of overhead per 256 KiB column row).  Pinned
+// and registered host memory is mapped for the GPU, so one launch per slice
+// reads every row over PCIe instead.  The host only hands over rows that lie
+// inside one HIP-known host allocation, 16-B aligned at both ends of the
+// dwordx4 body; the last len % 16 bytes go byte by byte, so nothing past a
+// row is read.  One workgroup per row; 4 loads of 16 B in flight per thread.
+struct GatherRow {
+  const uint8_t* src;  // device-visible address of the host bytes
+  uint8_t* dst;        // staging segment (256-B aligned)
+  uint64_t len;
+};
+
+extern "C" __global__ __launch_bounds__(256) void qsmd5_gather_kernel(const GatherRow* __restrict__ rows,
+                                                                     uint32_t nrows) {
+  const uint32_t r = blockIdx.x;
+  if (r >= nrows) return;
+  const GatherRow g = rows[r];
+  const uint64_t nvec = g.len >> 4;
+  const u32x4* __restrict__ src = reinterpret_cast<const u32x4*>(g.src);
+  u32x4* __restrict__ dst = reinterpret_cast<u32x4*>(g.dst);
+  constexpr uint32_t kU = 4;
+  uint64_t i = threadIdx.x;
+  for (; i + (kU - 1) * 256u < nvec; i += kU * 256u) {
+    u32x4 v[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) v[u] = __builtin_nontemporal_load(src + i + u * 256u);
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) dst[i + u * 256u] = v[u];
+  }
+  for (; i < nvec; i += 256u) dst[i] = __builtin_nontemporal_load(src + i);
+  const uint64_t tail = g.len & 15u;
+  if (threadIdx.x < tail) g.dst[(nvec << 4) + threadIdx.x] = g.src[(nvec << 4) + threadIdx.x];
+}
+
+// ---------------------------------------------------------------------------
 // Host launchers (md5_launch.h).
 #include "md5_launch.h"
 
@@ -802,6 +840,13 @@ hipError_t launch_column(const void* segs, const uint32_t* order, uint32_t n, ui
   return hipGetLastError();
 }
 
+
+hipError_t launch_gather(const void* rows, uint32_t nrows, hipStream_t s) {
+  if (nrows == 0) return hipSuccess;
+  hipLaunchKernelGGL(qsmd5_gather_kernel, dim3(nrows), dim3(256), 0, s,
+                     static_cast<const GatherRow*>(rows), nrows);
+  return hipGetLastError();
+}
 
 hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint64_t total_len,
                         hipStream_t s) {

@@ -384,6 +384,30 @@ class Classifier {
     return it != vmas_.begin() && lo < (it - 1)->hi && hi <= (it - 1)->hi;
   }
 
+  // Does [lo, hi) lie inside ONE pinned or registered host allocation?  Then a
+  // kernel may read it over PCIe (qsmd5_gather_kernel); *dev is the
+  // device-visible address of lo.  Exact, like span_in_one, and independent of
+  // QSMD5_FLAG_HOST: a device pointer or pageable memory answers false.
+  bool hip_host_range(uintptr_t lo, uintptr_t hi, uintptr_t* dev) {
+    if (hi <= lo || !span_in_one(lo, hi)) return false;
+    for (int k = 0; k < used_; ++k) {
+      Range& r = ranges_[(next_ + kRanges - 1 - k) % kRanges];
+      if (!r.hip || lo - r.lo >= r.size) continue;
+      if (r.kind != kHostMem) return false;
+      if (!r.dev) {
+        void* d = nullptr;
+        if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(r.lo), 0) != hipSuccess || !d) {
+          (void)hipGetLastError();
+          return false;
+        }
+        r.dev = reinterpret_cast<uintptr_t>(d);
+      }
+      *dev = r.dev + (lo - r.lo);
+      return true;
+    }
+    return false;  // pageable: span_in_one found it in a host VMA
+  }
+
  private:
   // Parse the maps only after this many pageable queries in one batch: by then
   // the queries have cost (70-260 ns each) about what one parse of a large
@@ -393,7 +417,7 @@ class Classifier {
     uintptr_t lo, hi;
   };
   void remember(uintptr_t lo, size_t size, MemKind kind, int owner, bool hip) {
-    ranges_[next_] = Range{lo, size, kind, owner, hip};
+    ranges_[next_] = Range{lo, size, kind, owner, hip, 0};
     next_ = (next_ + 1) % kRanges;
     used_ = used_ < kRanges ? used_ + 1 : kRanges;
   }
@@ -414,7 +438,8 @@ class Classifier {
     size_t size;
     MemKind kind;
     int owner;
-    bool hip;  // an exact HIP allocation (else a host VMA)
+    bool hip;        // an exact HIP allocation (else a host VMA)
+    uintptr_t dev;   // pinned/registered host allocation: device-visible address of lo (0: unknown)
   };
   static constexpr int kRanges = 8;
   Range ranges_[kRanges] = {};
@@ -555,14 +580,50 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   if (!slices.empty() && !inline_data)
     if (int rc = r.d_staging.reserve(nregions * region)) return rc;
 
+  // H2D copies of each slice (qsmd5_plan.h plan_copy_runs): runs of rows in one
+  // allocation at a constant stride go as one 2-D copy.  Rows left on their
+  // own that sit in a pinned or registered host allocation (a pool of pinned
+  // buffers, each its own allocation) are gathered by ONE qsmd5_gather_kernel
+  // launch per slice instead of one hipMemcpyAsync each (QSMD5_GATHER=0: off).
+  std::vector<std::vector<qsmd5::CopyRun>> slice_runs(inline_data ? 0 : slices.size());
+  std::vector<uintptr_t> gather_dev(inline_data ? 0 : host_idx.size(), 0);  // 0: not gatherable
+  if (!inline_data && !slices.empty()) {
+    if (env_u64("QSMD5_GATHER", 1))
+      for (size_t k = 0; k < host_idx.size(); ++k) {
+        const uintptr_t p = reinterpret_cast<uintptr_t>(chunks[host_idx[k]].ptr);
+        uintptr_t dev = 0;
+        if ((p & 15u) == 0 && cls.hip_host_range(p, p + host_len[k], &dev)) gather_dev[k] = dev;
+      }
+    for (size_t si = 0; si < slices.size(); ++si) {
+      const qsmd5::Slice& sl = slices[si];
+      const qsmd5::Group& g = groups[sl.group];
+      const uint64_t col_off = W == kNoColumns ? 0 : (uint64_t)sl.col * W;
+      slice_runs[si] = qsmd5::plan_copy_runs(
+          sl.active,
+          [&](size_t k) {
+            return (uint64_t)reinterpret_cast<uintptr_t>(chunks[host_idx[g.first + k]].ptr) + col_off;
+          },
+          [&](size_t k) { return col_bytes(len[host_idx[g.first + k]], sl.col); },
+          [&](uint64_t lo, uint64_t hi) { return cls.span_in_one(lo, hi); });
+    }
+  }
+  auto gathered = [&](const qsmd5::Slice& sl, const qsmd5::CopyRun& run) {
+    return run.rows == 1 && gather_dev[groups[sl.group].first + run.first] != 0;
+  };
+  size_t ngather = 0;
+  for (size_t si = 0; si < slice_runs.size(); ++si)
+    for (const qsmd5::CopyRun& run : slice_runs[si]) ngather += gathered(slices[si], run);
+
   // One metadata block: descriptors (device pointers) for every chunk, then
   // segment descriptors of the multi-column slices; the lane->chunk maps; the
-  // inline data.
+  // gather rows; the inline data.
   const size_t meta_bytes = n * sizeof(qsmd5_chunk) + nseg * sizeof(qsmd5_chunk);
   const size_t order_words = n + nseg;
   const size_t desc_span = (meta_bytes + 255) & ~size_t(255);
   const size_t order_span = (order_words * sizeof(uint32_t) + 255) & ~size_t(255);
-  const size_t data_off = desc_span + order_span;
+  const size_t gather_off = desc_span + order_span;
+  const size_t gather_span = (ngather * qsmd5::kGatherRowBytes + 255) & ~size_t(255);
+  const size_t data_off = gather_off + gather_span;
   const size_t block_bytes = data_off + inline_bytes;
   if (int rc = r.h_meta.reserve(block_bytes + 256)) return rc;
   if (int rc = r.d_meta.reserve(block_bytes + 256)) return rc;
@@ -578,13 +639,16 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   uint32_t* hso = ho + n;
   for (size_t i = 0; i < n; ++i) hd[i] = {len[i] ? chunks[i].ptr : nullptr, len[i]};
   uint8_t* stage = inline_data ? dm + data_off : static_cast<uint8_t*>(r.d_staging.p);
+  size_t ngather_filled = 0;
   std::vector<uint8_t*> slice_base(slices.size());
+  std::vector<size_t> row_off;  // staged offset of each active row of the slice
   for (size_t si = 0; si < slices.size(); ++si) {
     const qsmd5::Slice& sl = slices[si];
     const qsmd5::Group& g = groups[sl.group];
     uint8_t* base = stage + (si % nregions) * region;
     slice_base[si] = base;
     uint64_t off = 0;
+    row_off.resize(sl.active);
     for (size_t k = 0; k < sl.active; ++k) {
       const uint32_t ci = host_idx[g.first + k];
       if (g.ncols > 1) {
@@ -594,7 +658,19 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
         hd[ci].ptr = base + off;
       }
       if (inline_data) memcpy(hm + data_off + off, chunks[ci].ptr, len[ci]);
+      row_off[k] = off;
       off += stage_bytes(col_bytes(len[ci], sl.col));
+    }
+    if (inline_data) continue;
+    const uint64_t col_off = W == kNoColumns ? 0 : (uint64_t)sl.col * W;
+    for (const qsmd5::CopyRun& run : slice_runs[si]) {
+      if (!gathered(sl, run)) continue;
+      const size_t k = run.first;
+      uint64_t* gr = reinterpret_cast<uint64_t*>(hm + gather_off) + 3 * ngather_filled;
+      gr[0] = gather_dev[g.first + k] + col_off;
+      gr[1] = reinterpret_cast<uint64_t>(base + row_off[k]);
+      gr[2] = col_bytes(len[host_idx[g.first + k]], sl.col);
+      ++ngather_filled;
     }
   }
   size_t pos = 0;
@@ -628,6 +704,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   const qsmd5_chunk* d_seg = d_desc + n;
   uint32_t* d_dig = static_cast<uint32_t*>(r.d_dig.p);
   bool first_kernel = true;
+  size_t gather_next = 0;  // gather rows launched so far (slices take them in order)
   unsigned used = 0;  // compute streams (1..) that ran work: joined into s0 at the end
   auto mark_first = [&](hipStream_t s) -> int {
     if (first_kernel) {
@@ -674,22 +751,19 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     const uint64_t col_off = W == kNoColumns ? 0 : (uint64_t)sl.col * W;
     uint8_t* dst = slice_base[si];
     if (trace) QS_HIP(hipEventRecord(tr[4 * si], cp));
-    // Runs of equal-length rows at a constant stride inside one allocation or
-    // mapping go as one 2-D copy (qsmd5_plan.h plan_copy_runs, CPU-tested in
-    // tests/cpp/test_plan.cpp); every other row is its own copy.
-    const std::vector<qsmd5::CopyRun> runs =
-        inline_data ? std::vector<qsmd5::CopyRun>()
-                    : qsmd5::plan_copy_runs(
-                          sl.active,
-                          [&](size_t k) {
-                            return (uint64_t)reinterpret_cast<uintptr_t>(chunks[host_idx[g.first + k]].ptr) +
-                                   col_off;
-                          },
-                          [&](size_t k) { return col_bytes(len[host_idx[g.first + k]], sl.col); },
-                          [&](uint64_t lo, uint64_t hi) { return cls.span_in_one(lo, hi); });
+    // The slice's copies (planned above): 2-D runs and single rows by DMA,
+    // gathered rows by one kernel launch.
+    size_t slice_gather = 0;
+    static const std::vector<qsmd5::CopyRun> kNoRuns;  // inline data: already in the meta copy
+    const std::vector<qsmd5::CopyRun>& runs = inline_data ? kNoRuns : slice_runs[si];
     for (const qsmd5::CopyRun& run : runs) {
       const uint32_t ci = host_idx[g.first + run.first];
       const uint64_t w = col_bytes(len[ci], sl.col);
+      if (gathered(sl, run)) {
+        ++slice_gather;
+        dst += stage_bytes(w);
+        continue;
+      }
       const uint8_t* src = static_cast<const uint8_t*>(chunks[ci].ptr) + col_off;
       hipError_t e = hipSuccess;
       if (run.rows > 1) {
@@ -709,6 +783,15 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       }
       if (e != hipSuccess) return drain(hip_fail(e, "hipMemcpyAsync H2D"));
       dst += run.rows * stage_bytes(w);
+    }
+    if (slice_gather) {
+      // the gather rows live in the metadata block copied on s0
+      hipError_t e = one_stream ? hipSuccess : hipStreamWaitEvent(cp, r.ev_meta, 0);
+      if (e == hipSuccess)
+        e = qsmd5::launch_gather(dm + gather_off + gather_next * qsmd5::kGatherRowBytes,
+                                 (uint32_t)slice_gather, cp);
+      if (e != hipSuccess) return drain(hip_fail(e, "qsmd5 gather launch"));
+      gather_next += slice_gather;
     }
     if (trace) QS_HIP(hipEventRecord(tr[4 * si + 1], cp));
     hipError_t e = hipSuccess;

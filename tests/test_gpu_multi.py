@@ -128,3 +128,25 @@ sys.exit(0 if (rc == 0 if want == "None" else rc == -getattr(errno, want)) else 
     out = subprocess.run([PY, "-c", script, str(errno_name)], env=e, capture_output=True, text=True,
                          timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr[-2000:]
+
+
+def test_part_count_beyond_one_gpu_shards():
+    """North star: shard "only when one file's part count exceeds a single
+    GPU's batch".  40 000 small host parts (4 MB, far below QSMD5_SHARD_BYTES)
+    exceed one GPU's 32 768 resident chains, so both contexts take a shard."""
+    script = r'''
+import ctypes
+import qsmd5
+from oracle_util import lcg_bytes, md5_many
+n, L = 40000, 100
+buf = lcg_bytes(31, n * L)
+chunks = [(ctypes.addressof(buf) + i * L, L - (i % 3)) for i in range(n)]
+assert qsmd5.hash_batch(chunks) == md5_many(chunks)
+print("parts-ok")
+'''
+    out = _run(script, QSMD5_DEVICES="0,0", QSMD5_TRACE="1")
+    assert out.returncode == 0, out.stdout + out.stderr[-4000:]
+    assert "parts-ok" in out.stdout
+    shards = [l for l in out.stderr.splitlines() if l.startswith("qsmd5 shard:")]
+    assert any("context 1 (GPU 0) takes" in l and not l.endswith("takes 0 chunks") for l in shards), \
+        "\n".join(shards)

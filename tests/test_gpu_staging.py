@@ -169,3 +169,31 @@ def test_file_parts_in_one_buffer_still_one_run(pinned):
     chunks = [(pinned + i * L, L) for i in range(SIZE // L)]
     _check(chunks)
     _check(chunks, column=256 << 10)
+
+
+@pytest.mark.parametrize("gather", ["1", "0"])
+@pytest.mark.parametrize("column", [None, 1024, 4160])
+def test_gather_kernel_rows_from_pinned_buffers(pinned, gather, column, monkeypatch):
+    """Rows that cannot share a 2-D copy and sit in pinned memory are read by
+    qsmd5_gather_kernel (one launch per slice; QSMD5_GATHER=0 sends them back
+    to one DMA copy each).  16-B-aligned starts with every tail length 0..15,
+    rows shorter than 16 B, and separate pinned allocations."""
+    monkeypatch.setenv("QSMD5_GATHER", gather)
+    others = [qsmd5.alloc_pinned(1 << 20) for _ in range(3)]
+    try:
+        for i, o in enumerate(others):
+            _fill_n(o, 1 << 20, 10 + i)
+        chunks = []
+        for i, L in enumerate([1, 15, 16, 17, 31, 4096 + 5, 65536 + 15, 300000 + 7]):
+            base = others[i % 3] if i % 2 else pinned
+            chunks.append((base + 16 * (1 + 7 * i), L))  # 16-B aligned, irregular spacing
+        chunks += [(o + 16 * 5, 200003) for o in others]  # equal lengths, separate allocations
+        _check(chunks, column=column)
+    finally:
+        for o in others:
+            qsmd5.free_pinned(o)
+
+
+def _fill_n(ptr, n, seed):
+    a = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(ptr))
+    a[:] = np.random.default_rng(seed).integers(0, 256, size=n, dtype=np.uint8)
