@@ -767,18 +767,21 @@ extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_coal_kernel(
 // reads every row over PCIe instead.  The host only hands over rows that lie
 // inside one HIP-known host allocation, 16-B aligned at both ends of the
 // dwordx4 body; the last len % 16 bytes go byte by byte, so nothing past a
-// row is read.  One workgroup per row; 4 loads of 16 B in flight per thread.
+// row is read.  A few persistent workgroups walk the rows: 8 of them, with 4
+// loads of 16 B in flight per thread (128 KiB in flight), keep the link full,
+// as 4 already do.  More hurt: the chains of earlier columns run beside the
+// gathers of later ones, and with one workgroup per row their 2 ms columns
+// took up to 94 ms, with 64 workgroups 5-6 ms -- the chains' HBM loads queue
+// behind the gathers' PCIe reads.  8 workgroups leave them at 2.05-2.1 ms
+// (profiles/r02_gather_groups.log).  Each also reserves 80 KiB of LDS it never
+// uses, so a CU holding one cannot take a latency-kernel workgroup (128 KiB).
 struct GatherRow {
   const uint8_t* src;  // device-visible address of the host bytes
   uint8_t* dst;        // staging segment (256-B aligned)
   uint64_t len;
 };
 
-extern "C" __global__ __launch_bounds__(256) void qsmd5_gather_kernel(const GatherRow* __restrict__ rows,
-                                                                     uint32_t nrows) {
-  const uint32_t r = blockIdx.x;
-  if (r >= nrows) return;
-  const GatherRow g = rows[r];
+__device__ __forceinline__ void gather_row(const GatherRow g) {
   const uint64_t nvec = g.len >> 4;
   const u32x4* __restrict__ src = reinterpret_cast<const u32x4*>(g.src);
   u32x4* __restrict__ dst = reinterpret_cast<u32x4*>(g.dst);
@@ -794,6 +797,11 @@ extern "C" __global__ __launch_bounds__(256) void qsmd5_gather_kernel(const Gath
   for (; i < nvec; i += 256u) dst[i] = __builtin_nontemporal_load(src + i);
   const uint64_t tail = g.len & 15u;
   if (threadIdx.x < tail) g.dst[(nvec << 4) + threadIdx.x] = g.src[(nvec << 4) + threadIdx.x];
+}
+
+extern "C" __global__ __launch_bounds__(256) void qsmd5_gather_kernel(const GatherRow* __restrict__ rows,
+                                                                     uint32_t nrows) {
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) gather_row(rows[r]);
 }
 
 // ---------------------------------------------------------------------------
@@ -841,10 +849,12 @@ hipError_t launch_column(const void* segs, const uint32_t* order, uint32_t n, ui
 }
 
 
-hipError_t launch_gather(const void* rows, uint32_t nrows, hipStream_t s) {
+hipError_t launch_gather(const void* rows, uint32_t nrows, hipStream_t s, uint32_t groups) {
   if (nrows == 0) return hipSuccess;
-  hipLaunchKernelGGL(qsmd5_gather_kernel, dim3(nrows), dim3(256), 0, s,
-                     static_cast<const GatherRow*>(rows), nrows);
+  constexpr size_t kGatherLds = 80u << 10;  // keeps latency-kernel workgroups off these CUs
+  if (groups == 0) groups = 1;
+  hipLaunchKernelGGL(qsmd5_gather_kernel, dim3(nrows < groups ? nrows : groups),
+                     dim3(256), kGatherLds, s, static_cast<const GatherRow*>(rows), nrows);
   return hipGetLastError();
 }
 

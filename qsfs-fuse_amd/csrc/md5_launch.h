@@ -45,7 +45,7 @@ hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint
 // Gather rows {src (device-visible host address), dst (staging), len} into the
 // staging ring, one workgroup per row; rows: device array of 24-B records.
 constexpr size_t kGatherRowBytes = 24;
-hipError_t launch_gather(const void* rows, uint32_t nrows, hipStream_t s);
+hipError_t launch_gather(const void* rows, uint32_t nrows, hipStream_t s, uint32_t groups);
 hipError_t warm_up(hipStream_t s);
 hipError_t launch_lcg_fill(uint8_t* base, uint64_t stride, uint64_t len, uint32_t seed0,
                            uint32_t nchunks, hipStream_t s);

@@ -789,7 +789,8 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       hipError_t e = one_stream ? hipSuccess : hipStreamWaitEvent(cp, r.ev_meta, 0);
       if (e == hipSuccess)
         e = qsmd5::launch_gather(dm + gather_off + gather_next * qsmd5::kGatherRowBytes,
-                                 (uint32_t)slice_gather, cp);
+                                 (uint32_t)slice_gather, cp,
+                                 (uint32_t)env_u64("QSMD5_GATHER_GROUPS", 8));
       if (e != hipSuccess) return drain(hip_fail(e, "qsmd5 gather launch"));
       gather_next += slice_gather;
     }
