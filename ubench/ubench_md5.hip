@@ -149,6 +149,14 @@ __global__ __launch_bounds__(128) void k_chain_cost(uint64_t* out, uint32_t* sin
   sink[lane] = st[0] ^ st[1] ^ st[2] ^ st[3];
 }
 
+// Latency kernel with 5-block phases: a 160 KiB ring (all of a gfx950 CU's
+// LDS), one barrier per 5 blocks instead of per 4.
+__global__ __launch_bounds__(128) void k_pc_half5(const ChunkDesc* __restrict__ c,
+                                                  const uint32_t* __restrict__ o, uint32_t n,
+                                                  uint32_t* __restrict__ d, uint32_t skew) {
+  pc_body<false, 1, 5>(c, o, n, d, 0, ~0ull, nullptr, skew);
+}
+
 // Coalesced kernel with immediate-offset DMA in the fast region.
 __global__ __launch_bounds__(64) void k_coal_imm(const ChunkDesc* __restrict__ c,
                                                  const uint32_t* __restrict__ o, uint32_t n,
@@ -356,6 +364,9 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 6)
       hipLaunchKernelGGL(k_coal_imm, dim3(grid), dim3(64), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig);
+    else if (which == 7)
+      hipLaunchKernelGGL(k_pc_half5, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, 0u);
 
     else
       hipLaunchKernelGGL(k_pc_depth<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
@@ -461,7 +472,9 @@ static int run_edges(int which) {
   else if (which == 6)
     hipLaunchKernelGGL(k_coal_imm, dim3((n + 63) / 64), dim3(64), 0, 0, dd, nullptr, (uint32_t)n,
                        dg);
-
+  else if (which == 7)
+    hipLaunchKernelGGL(k_pc_half5, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr, (uint32_t)n,
+                       dg, 0u);
   else
     hipLaunchKernelGGL(k_pc_depth<3>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew);
@@ -1002,6 +1015,16 @@ int main(int argc, char** argv) {
     CK(hipFree(d_dig));
     CK(hipFree(d_tr));
     return 0;
+  }
+  if (!strcmp(mode, "half5")) {
+    // A/B/A/B: 4-block phases (128 KiB ring) vs 5-block phases (160 KiB ring)
+    int bad = 0;
+    bad += run_edges(7);
+    for (int rep = 0; rep < 2; ++rep) {
+      run_md5(512, 10ull << 20, 5, rep == 0, 1);
+      run_md5(512, 10ull << 20, 5, rep == 0, 7);
+    }
+    return bad ? 1 : 0;
   }
   if (!strcmp(mode, "chaincost")) {
     // cycles per 64-B block of the chain wave, by what it does besides the steps
