@@ -183,6 +183,17 @@ QSMD5_API void qsmd5_ctx_destroy(qsmd5_ctx* ctx);
 QSMD5_API int qsmd5_alloc_pinned(size_t bytes, void** out);
 QSMD5_API int qsmd5_free_pinned(void* ptr);
 
+/* Register existing host buffers with the GPU (hipHostRegister), e.g. qsfs's
+ * transfer-buffer pool once at start-up (TransferManager::InitializeResources,
+ * TransferManager.cpp:103-108): their pages are then locked once instead of on
+ * each batch's first touch, and rows in separate registered buffers are
+ * gathered by one kernel per column.  The range is widened to
+ * whole pages.  Unregister (with the same ptr) before freeing the memory.
+ * -EINVAL for a NULL/empty range, a ptr registered twice, or unregistering a
+ * ptr this library did not register. */
+QSMD5_API int qsmd5_register_host(void* ptr, size_t bytes);
+QSMD5_API int qsmd5_unregister_host(void* ptr);
+
 /* Part slicing identical to QSTransferManager::PrepareUpload
  * (QSTransferManager.cpp:492-546): a single part below `threshold`, else
  * parts of `buf_size` with the last two averaged when the remainder is below

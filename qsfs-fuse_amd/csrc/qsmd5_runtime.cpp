@@ -28,6 +28,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <map>
 #include <mutex>
 #include <new>
 #include <numeric>
@@ -845,8 +846,9 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     fprintf(stderr, "qsmd5 trace: %zu chunks: classify %.2f ms, sort %.2f ms, plan %.2f ms, "
             "enqueue+run %.2f ms\n", n, ms(t0, t_classified), ms(t_classified, t_sorted),
             ms(t_sorted, t_planned), ms(t_planned, t_end));
-    fprintf(stderr, "qsmd5 trace: %zu slices, column width %llu, %zu groups, %zu regions\n",
-            slices.size(), (unsigned long long)(W == kNoColumns ? 0 : W), groups.size(), nregions);
+    fprintf(stderr, "qsmd5 trace: %zu slices, column width %llu, %zu groups, %zu regions, "
+            "%zu gathered rows\n", slices.size(), (unsigned long long)(W == kNoColumns ? 0 : W),
+            groups.size(), nregions, ngather);
     for (size_t si = 0; si < slices.size(); ++si) {
       float t[4] = {0, 0, 0, 0};
       for (int k = 0; k < 4; ++k) (void)hipEventElapsedTime(&t[k], tr.back(), tr[4 * si + k]);
@@ -1515,6 +1517,39 @@ int qsmd5_free_pinned(void* ptr) {
     if (!ptr) return 0;
     if (int rc = ensure_init()) return rc;
     QS_HIP(hipHostFree(ptr));
+    return 0;
+  });
+}
+
+// Registered ranges are widened to whole pages (a malloc'd vector<char> starts
+// 16 B into its mapping); the page-aligned base is what HIP unregisters.
+static std::mutex g_reg_mu;
+static std::map<uintptr_t, uintptr_t>* g_reg = new std::map<uintptr_t, uintptr_t>;  // user -> base
+
+int qsmd5_register_host(void* ptr, size_t bytes) {
+  return guarded([&] {
+    if (!ptr || !bytes) return fail(-EINVAL, "qsmd5: NULL or empty range to register");
+    if (int rc = ensure_init()) return rc;
+    const uintptr_t page = 4096, u = reinterpret_cast<uintptr_t>(ptr);
+    const uintptr_t lo = u & ~(page - 1), hi = (u + bytes + page - 1) & ~(page - 1);
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    if (g_reg->count(u)) return fail(-EINVAL, "qsmd5: range already registered");
+    QS_HIP(hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault));
+    (*g_reg)[u] = lo;
+    return 0;
+  });
+}
+
+int qsmd5_unregister_host(void* ptr) {
+  return guarded([&] {
+    if (!ptr) return fail(-EINVAL, "qsmd5: NULL pointer to unregister");
+    if (int rc = ensure_init()) return rc;
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    auto it = g_reg->find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == g_reg->end()) return fail(-EINVAL, "qsmd5: pointer was not registered by qsmd5_register_host");
+    const uintptr_t base = it->second;
+    g_reg->erase(it);
+    QS_HIP(hipHostUnregister(reinterpret_cast<void*>(base)));
     return 0;
   });
 }

@@ -22,7 +22,7 @@ import os
 __all__ = [
     "Md5Error", "lib", "lib_path", "hexdigest", "md5", "md5_stream", "MD5", "hash_batch",
     "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
-    "alloc_pinned", "free_pinned", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
+    "alloc_pinned", "free_pinned", "register_host", "unregister_host", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
     "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST", "FLAG_GPU_ONLY",
     "FLAG_CPU_ONLY", "stats", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU",
 ]
@@ -115,6 +115,8 @@ def lib():
         "qsmd5_ctx_destroy": (None, [ctypes.c_void_p]),
         "qsmd5_alloc_pinned": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
         "qsmd5_free_pinned": (ctypes.c_int, [ctypes.c_void_p]),
+        "qsmd5_register_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
+        "qsmd5_unregister_host": (ctypes.c_int, [ctypes.c_void_p]),
         "qsmd5_plan_parts": (ctypes.c_int, [ctypes.c_uint64] * 5 + [
             ctypes.POINTER(Part), ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]),
         "qsmd5_hash_parts": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(Part), ctypes.c_size_t,
@@ -392,6 +394,14 @@ def alloc_pinned(nbytes):
 
 def free_pinned(ptr):
     _check(lib().qsmd5_free_pinned(ctypes.c_void_p(ptr)), "qsmd5_free_pinned")
+
+
+def register_host(ptr, nbytes):
+    _check(lib().qsmd5_register_host(ctypes.c_void_p(ptr), nbytes), "qsmd5_register_host")
+
+
+def unregister_host(ptr):
+    _check(lib().qsmd5_unregister_host(ctypes.c_void_p(ptr)), "qsmd5_unregister_host")
 
 
 def synth_fill_lcg(base_ptr, stride, length, seed0, nchunks, stream=0):

@@ -59,3 +59,18 @@ def test_default_pool_routes_waves_by_size(gold):
     assert small["md5"] == gold[:64] and big["md5"] == gold[:128]
     print("64 parts, pool 5 (CPU waves): hash %.3f s; 128 parts, pool 64 (GPU waves): hash %.3f s"
           % (small["hash_s"], big["hash_s"]))
+
+
+@pytest.mark.gpu
+def test_registered_pageable_pool(gold):
+    """qsfs's own pageable buffers, registered once (qsmd5_register_host, as
+    at daemon start-up): no first-touch page locking, and the separate buffers'
+    rows go through the gather kernel."""
+    r = run(["--aligned", "--size=%d" % (512 * 10 * MiB), "--pool=512", "--register", "--repeat=2"],
+            "gpu")
+    assert r["registered"] and r["gpu_waves"] == 1
+    assert r["md5"] == gold[:512]
+    first, warm = r["hash_s_runs"]
+    print("512 x 10 MiB, 512 registered pageable buffers: register %.3f s once; hash first pass "
+          "%.3f s (%.1f GiB/s), reused %.3f s (%.1f GiB/s)"
+          % (r["register_s"], first, 5.0 / first, warm, 5.0 / warm))

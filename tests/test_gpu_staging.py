@@ -197,3 +197,20 @@ def test_gather_kernel_rows_from_pinned_buffers(pinned, gather, column, monkeypa
 def _fill_n(ptr, n, seed):
     a = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(ptr))
     a[:] = np.random.default_rng(seed).integers(0, 256, size=n, dtype=np.uint8)
+
+
+def test_gather_from_registered_pageable_buffers(pinned):
+    """Pageable buffers registered with qsmd5_register_host are HIP-known host
+    memory: rows in separate registered buffers take the gather kernel."""
+    bufs = [np.zeros(SIZE // 4, dtype=np.uint8) for _ in range(3)]
+    for i, b in enumerate(bufs):
+        b[:] = np.random.default_rng(40 + i).integers(0, 256, size=b.size, dtype=np.uint8)
+        qsmd5.register_host(b.ctypes.data, b.nbytes)
+    try:
+        L = (1 << 20) + 9
+        chunks = [(b.ctypes.data + 16 * k, L) for k in range(2) for b in bufs]
+        _check(chunks)
+        _check(chunks, column=4160)
+    finally:
+        for b in bufs:
+            qsmd5.unregister_host(b.ctypes.data)
