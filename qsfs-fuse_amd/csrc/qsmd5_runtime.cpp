@@ -315,6 +315,31 @@ MemKind classify(const void* p, int* owner = nullptr, bool* hip_known = nullptr)
 //   answers "host", so it can never send a host pointer to a kernel.
 // A batch's chunks mostly sit in a few allocations (a pool, a file buffer,
 // torch's caching allocator).  QSMD5_FLAG_HOST skips all queries.
+// Host ranges registered through qsmd5_register_host, widened to whole pages
+// (a malloc'd vector<char> starts 16 B into its mapping).  HIP's
+// hipMemGetAddressRange does not describe registered memory, so the
+// classifier takes their exact extent from here (leaked, as rt()).
+struct Registry {
+  std::mutex mu;
+  std::map<uintptr_t, uintptr_t> base_of;  // user pointer -> page-aligned base
+  std::map<uintptr_t, uintptr_t> end_of;   // page-aligned base -> end
+  // The registered range holding p, if any: [*lo, *hi).
+  bool find(uintptr_t p, uintptr_t* lo, uintptr_t* hi) {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = end_of.upper_bound(p);
+    if (it == end_of.begin()) return false;
+    --it;
+    if (p >= it->second) return false;
+    *lo = it->first;
+    *hi = it->second;
+    return true;
+  }
+};
+Registry& registry() {
+  static Registry* r = new Registry;
+  return *r;
+}
+
 class Classifier {
  public:
   Classifier(int flags, size_t n)
@@ -370,12 +395,17 @@ class Classifier {
     if (hip_known) {
       hipDeviceptr_t base = nullptr;
       size_t size = 0;
-      if (hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(lo)) != hipSuccess || !size) {
+      uintptr_t b = 0;
+      if (hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(lo)) == hipSuccess && size &&
+          lo - reinterpret_cast<uintptr_t>(base) < size) {
+        b = reinterpret_cast<uintptr_t>(base);
+      } else {
         (void)hipGetLastError();
-        return false;
+        uintptr_t rlo = 0, rhi = 0;  // memory registered through qsmd5_register_host
+        if (owner >= 0 || !registry().find(lo, &rlo, &rhi)) return false;
+        b = rlo;
+        size = rhi - rlo;
       }
-      const uintptr_t b = reinterpret_cast<uintptr_t>(base);
-      if (lo - b >= size) return false;
       remember(b, size, owner >= 0 ? kDeviceMem : kHostMem, owner, true);
       return hi - b <= size;
     }
@@ -1521,10 +1551,6 @@ int qsmd5_free_pinned(void* ptr) {
   });
 }
 
-// Registered ranges are widened to whole pages (a malloc'd vector<char> starts
-// 16 B into its mapping); the page-aligned base is what HIP unregisters.
-static std::mutex g_reg_mu;
-static std::map<uintptr_t, uintptr_t>* g_reg = new std::map<uintptr_t, uintptr_t>;  // user -> base
 
 int qsmd5_register_host(void* ptr, size_t bytes) {
   return guarded([&] {
@@ -1532,10 +1558,13 @@ int qsmd5_register_host(void* ptr, size_t bytes) {
     if (int rc = ensure_init()) return rc;
     const uintptr_t page = 4096, u = reinterpret_cast<uintptr_t>(ptr);
     const uintptr_t lo = u & ~(page - 1), hi = (u + bytes + page - 1) & ~(page - 1);
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    if (g_reg->count(u)) return fail(-EINVAL, "qsmd5: range already registered");
+    Registry& R = registry();
+    std::lock_guard<std::mutex> lk(R.mu);
+    if (R.base_of.count(u) || R.end_of.count(lo))
+      return fail(-EINVAL, "qsmd5: range already registered");
     QS_HIP(hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault));
-    (*g_reg)[u] = lo;
+    R.base_of[u] = lo;
+    R.end_of[lo] = hi;
     return 0;
   });
 }
@@ -1544,11 +1573,14 @@ int qsmd5_unregister_host(void* ptr) {
   return guarded([&] {
     if (!ptr) return fail(-EINVAL, "qsmd5: NULL pointer to unregister");
     if (int rc = ensure_init()) return rc;
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    auto it = g_reg->find(reinterpret_cast<uintptr_t>(ptr));
-    if (it == g_reg->end()) return fail(-EINVAL, "qsmd5: pointer was not registered by qsmd5_register_host");
+    Registry& R = registry();
+    std::lock_guard<std::mutex> lk(R.mu);
+    auto it = R.base_of.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == R.base_of.end())
+      return fail(-EINVAL, "qsmd5: pointer was not registered by qsmd5_register_host");
     const uintptr_t base = it->second;
-    g_reg->erase(it);
+    R.base_of.erase(it);
+    R.end_of.erase(base);
     QS_HIP(hipHostUnregister(reinterpret_cast<void*>(base)));
     return 0;
   });

@@ -63,6 +63,8 @@ class BufferSlab {
   }
   BufferSlab(const BufferSlab&) = delete;
   BufferSlab& operator=(const BufferSlab&) = delete;
+  char* data() const { return base_; }
+  size_t bytes() const { return count_ * size_; }
   std::vector<PoolBuffer> buffers() const {
     std::vector<PoolBuffer> v;
     for (size_t k = 0; k < count_; ++k) v.push_back(PoolBuffer{base_ + k * size_, size_});

@@ -153,7 +153,10 @@ int main(int argc, char** argv) {
   double register_s = 0;
   if (reg && !pinned) {
     const auto r0 = std::chrono::steady_clock::now();
-    for (auto& b : pool)
+    // one registration per allocation: the slab at once, else each buffer
+    std::vector<qsmd5::PoolBuffer> regs =
+        slab ? std::vector<qsmd5::PoolBuffer>{{slab_pool->data(), slab_pool->bytes()}} : pool;
+    for (auto& b : regs)
       if (qsmd5_register_host(b.data, b.size)) {
         fprintf(stderr, "qsmd5_register_host: %s\n", qsmd5_last_error());
         return 1;
@@ -181,8 +184,11 @@ int main(int argc, char** argv) {
   }
   if (pinned && !slab)
     for (auto& b : pool) qsmd5_free_pinned(b.data);
-  if (reg && !pinned)
-    for (auto& b : pool) qsmd5_unregister_host(b.data);
+  if (reg && !pinned) {
+    if (slab) qsmd5_unregister_host(slab_pool->data());
+    else
+      for (auto& b : pool) qsmd5_unregister_host(b.data);
+  }
   printf("{\"size\": %llu, \"parts\": %zu, \"pages\": %zu, \"pool\": %zu, \"pinned\": %s, "
          "\"slab\": %s, \"registered\": %s, \"register_s\": %.6f, \"waves\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"seconds\": %.6f, "
          "\"gather_s\": %.6f, \"hash_s\": %.6f, \"upload_s\": %.6f, \"part_sizes\": [",
