@@ -27,11 +27,16 @@ REPORT_MARKERS = ("WARNING: ThreadSanitizer", "ERROR: AddressSanitizer", "runtim
                   "ERROR: LeakSanitizer")
 
 
-def _run(variant, devices, threads=6, rounds=12, max_len=3 << 20, extra=(), expect_clean=True):
+def _run(variant, devices, threads=6, rounds=12, max_len=3 << 20, extra=(), expect_clean=True,
+         backend="gpu", inject=None):
     exe = os.path.join(SAN, "race_stress_" + variant)
     if not os.path.exists(exe):
         pytest.fail("%s missing: run scripts/build_sanitized.sh (built by __graft_entry__.build())" % exe)
     env = dict(os.environ)
+    env["QSMD5_BACKEND"] = backend
+    env.pop("QSMD5_INJECT_GPU_FAULT", None)
+    if inject:
+        env["QSMD5_INJECT_GPU_FAULT"] = inject
     env.pop("QSMD5_DEVICES", None)
     if devices:
         env["QSMD5_DEVICES"] = devices
@@ -65,6 +70,18 @@ def test_race_stress_tsan(devices):
 @pytest.mark.parametrize("devices", ["", "0,0"])
 def test_race_stress_asan_ubsan(devices):
     print(_run("asan", devices))
+
+
+@pytest.mark.gpu
+@pytest.mark.cpu_backend
+@pytest.mark.parametrize("variant", ["tsan", "asan"])
+@pytest.mark.parametrize("inject", [None, "1"], ids=["routed", "gpu_fault_fallback"])
+def test_race_stress_auto_backend(variant, inject):
+    """QSMD5_BACKEND=auto: small calls and streams route to the library's CPU
+    MD5 (its helper threads included) while larger batches take the GPU; with
+    an injected GPU fault every GPU call falls back to the CPU.  Both under
+    the sanitizers, every digest against the oracle."""
+    print(_run(variant, "", backend="auto", inject=inject))
 
 
 @pytest.mark.gpu
