@@ -345,27 +345,30 @@ class Classifier {
   Classifier(int flags, size_t n)
       : all_host_(flags & QSMD5_FLAG_HOST),
         maps_after_(n >= 2 ? env_u64("QSMD5_MAPS_AFTER", kMapsAfter) : ~0ull) {}
-  MemKind operator()(const void* p, int* owner) {
+  // *hip (optional): 1 = HIP-known memory (device, pinned, registered); 0 =
+  // pageable as far as the caches tell (a registered subrange of a cached VMA
+  // reads as 0: it then just misses the gather kernel); 2 = not classified
+  // (QSMD5_FLAG_HOST).
+  MemKind operator()(const void* p, int* owner, uint8_t* hip = nullptr) {
     *owner = -1;
+    if (hip) *hip = all_host_ ? 2 : 0;
     if (all_host_ || !p) return kHostMem;
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     for (int k = 0; k < used_; ++k) {
       const Range& r = ranges_[(next_ + kRanges - 1 - k) % kRanges];  // newest first
       if (a - r.lo < r.size) {
         *owner = r.owner;
+        if (hip) *hip = r.hip ? 1 : 0;
         return r.kind;
       }
     }
     bool hip_known = false;
     const MemKind kind = classify(p, owner, &hip_known);
+    if (hip) *hip = hip_known ? 1 : 0;
     if (hip_known) {
-      hipDeviceptr_t base = nullptr;
+      uintptr_t lo = 0;
       size_t size = 0;
-      if (hipMemGetAddressRange(&base, &size, const_cast<void*>(p)) == hipSuccess && size &&
-          a - reinterpret_cast<uintptr_t>(base) < size)
-        remember(reinterpret_cast<uintptr_t>(base), size, kind, *owner, true);
-      else
-        (void)hipGetLastError();
+      if (hip_range(a, *owner, &lo, &size)) remember(lo, size, kind, *owner, true);
     } else if (kind == kHostMem && ++pageable_queries_ >= maps_after_) {
       if (!maps_read_) read_maps();
       auto it = std::upper_bound(vmas_.begin(), vmas_.end(), a,
@@ -393,19 +396,9 @@ class Classifier {
     bool hip_known = false;
     (void)classify(reinterpret_cast<const void*>(lo), &owner, &hip_known);
     if (hip_known) {
-      hipDeviceptr_t base = nullptr;
-      size_t size = 0;
       uintptr_t b = 0;
-      if (hipMemGetAddressRange(&base, &size, reinterpret_cast<void*>(lo)) == hipSuccess && size &&
-          lo - reinterpret_cast<uintptr_t>(base) < size) {
-        b = reinterpret_cast<uintptr_t>(base);
-      } else {
-        (void)hipGetLastError();
-        uintptr_t rlo = 0, rhi = 0;  // memory registered through qsmd5_register_host
-        if (owner >= 0 || !registry().find(lo, &rlo, &rhi)) return false;
-        b = rlo;
-        size = rhi - rlo;
-      }
+      size_t size = 0;
+      if (!hip_range(lo, owner, &b, &size)) return false;
       remember(b, size, owner >= 0 ? kDeviceMem : kHostMem, owner, true);
       return hi - b <= size;
     }
@@ -413,6 +406,26 @@ class Classifier {
     auto it = std::upper_bound(vmas_.begin(), vmas_.end(), lo,
                                [](uintptr_t x, const Vma& v) { return x < v.lo; });
     return it != vmas_.begin() && lo < (it - 1)->hi && hi <= (it - 1)->hi;
+  }
+
+  // The exact allocation holding HIP-known address a: hipMemGetAddressRange
+  // for HIP allocations, the library's registry for memory registered through
+  // qsmd5_register_host (which hipMemGetAddressRange does not describe).
+  static bool hip_range(uintptr_t a, int owner, uintptr_t* lo, size_t* size) {
+    hipDeviceptr_t base = nullptr;
+    size_t sz = 0;
+    if (hipMemGetAddressRange(&base, &sz, reinterpret_cast<void*>(a)) == hipSuccess && sz &&
+        a - reinterpret_cast<uintptr_t>(base) < sz) {
+      *lo = reinterpret_cast<uintptr_t>(base);
+      *size = sz;
+      return true;
+    }
+    (void)hipGetLastError();
+    uintptr_t rlo = 0, rhi = 0;
+    if (owner >= 0 || !registry().find(a, &rlo, &rhi)) return false;
+    *lo = rlo;
+    *size = rhi - rlo;
+    return true;
   }
 
   // Does [lo, hi) lie inside ONE pinned or registered host allocation?  Then a
@@ -539,6 +552,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
 
   std::vector<uint64_t> len(n);
   std::vector<MemKind> kind(n);
+  std::vector<uint8_t> hipk(n, 0);  // Classifier::operator() *hip of each chunk
   Classifier cls(flags, n);
   for (size_t i = 0; i < n; ++i) {
     uint64_t L = chunks[i].len;
@@ -547,7 +561,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     if (L > 0 && !chunks[i].ptr) return fail(-EINVAL, "qsmd5: NULL ptr with non-zero len");
     len[i] = L;
     int owner = -1;
-    kind[i] = L ? cls(chunks[i].ptr, &owner) : kDeviceMem;  // empty chunks read nothing
+    kind[i] = L ? cls(chunks[i].ptr, &owner, &hipk[i]) : kDeviceMem;  // empty chunks read nothing
     if (L && kind[i] == kDeviceMem && owner != r.device)
       return fail(-EINVAL, "qsmd5: chunk lives on GPU " + std::to_string(owner) +
                                ", not on a bound GPU (QSMD5_DEVICE/QSMD5_DEVICES)");
@@ -590,6 +604,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     column_bytes = (int64_t)env_u64("QSMD5_COLUMN_BYTES", 0);  // 0 = whole chunks
   const qsmd5::HostPlan plan =
       qsmd5::plan_host(host_len, r.staging_cap, env_u64("QSMD5_SLICE_BYTES", 0), column_bytes);
+  const auto t_hostplan = std::chrono::steady_clock::now();
   const uint64_t W = plan.W, region = plan.region;
   const std::vector<qsmd5::Group>& groups = plan.groups;
   const std::vector<qsmd5::Slice>& slices = plan.slices;
@@ -619,12 +634,6 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   std::vector<std::vector<qsmd5::CopyRun>> slice_runs(inline_data ? 0 : slices.size());
   std::vector<uintptr_t> gather_dev(inline_data ? 0 : host_idx.size(), 0);  // 0: not gatherable
   if (!inline_data && !slices.empty()) {
-    if (env_u64("QSMD5_GATHER", 1))
-      for (size_t k = 0; k < host_idx.size(); ++k) {
-        const uintptr_t p = reinterpret_cast<uintptr_t>(chunks[host_idx[k]].ptr);
-        uintptr_t dev = 0;
-        if ((p & 15u) == 0 && cls.hip_host_range(p, p + host_len[k], &dev)) gather_dev[k] = dev;
-      }
     for (size_t si = 0; si < slices.size(); ++si) {
       const qsmd5::Slice& sl = slices[si];
       const qsmd5::Group& g = groups[sl.group];
@@ -637,6 +646,26 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
           [&](size_t k) { return col_bytes(len[host_idx[g.first + k]], sl.col); },
           [&](uint64_t lo, uint64_t hi) { return cls.span_in_one(lo, hi); });
     }
+    // Gather candidates: rows left on their own (a file's parts or one pool
+    // slab form 2-D runs and never get here), in HIP-known or unclassified
+    // memory, 16-B aligned, the whole chunk in one pinned/registered host
+    // allocation.  Checked once per chunk.
+    if (env_u64("QSMD5_GATHER", 1)) {
+      std::vector<uint8_t> seen(host_idx.size(), 0);
+      for (size_t si = 0; si < slices.size(); ++si) {
+        const qsmd5::Group& g = groups[slices[si].group];
+        for (const qsmd5::CopyRun& run : slice_runs[si]) {
+          const size_t k = g.first + run.first;
+          if (run.rows != 1 || seen[k]) continue;
+          seen[k] = 1;
+          const uint32_t ci = host_idx[k];
+          const uintptr_t p = reinterpret_cast<uintptr_t>(chunks[ci].ptr);
+          uintptr_t dev = 0;
+          if (hipk[ci] != 0 && (p & 15u) == 0 && cls.hip_host_range(p, p + host_len[k], &dev))
+            gather_dev[k] = dev;
+        }
+      }
+    }
   }
   auto gathered = [&](const qsmd5::Slice& sl, const qsmd5::CopyRun& run) {
     return run.rows == 1 && gather_dev[groups[sl.group].first + run.first] != 0;
@@ -645,6 +674,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   for (size_t si = 0; si < slice_runs.size(); ++si)
     for (const qsmd5::CopyRun& run : slice_runs[si]) ngather += gathered(slices[si], run);
 
+  const auto t_runs = std::chrono::steady_clock::now();
   // One metadata block: descriptors (device pointers) for every chunk, then
   // segment descriptors of the multi-column slices; the lane->chunk maps; the
   // gather rows; the inline data.
@@ -679,7 +709,10 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     uint8_t* base = stage + (si % nregions) * region;
     slice_base[si] = base;
     uint64_t off = 0;
-    row_off.resize(sl.active);
+    bool any_gather = false;
+    if (!inline_data)
+      for (const qsmd5::CopyRun& run : slice_runs[si]) any_gather = any_gather || gathered(sl, run);
+    if (any_gather) row_off.resize(sl.active);
     for (size_t k = 0; k < sl.active; ++k) {
       const uint32_t ci = host_idx[g.first + k];
       if (g.ncols > 1) {
@@ -689,10 +722,10 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
         hd[ci].ptr = base + off;
       }
       if (inline_data) memcpy(hm + data_off + off, chunks[ci].ptr, len[ci]);
-      row_off[k] = off;
+      if (any_gather) row_off[k] = off;
       off += stage_bytes(col_bytes(len[ci], sl.col));
     }
-    if (inline_data) continue;
+    if (!any_gather) continue;
     const uint64_t col_off = W == kNoColumns ? 0 : (uint64_t)sl.col * W;
     for (const qsmd5::CopyRun& run : slice_runs[si]) {
       if (!gathered(sl, run)) continue;
@@ -873,9 +906,11 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       return std::chrono::duration<double, std::milli>(b - a).count();
     };
     const auto t_end = std::chrono::steady_clock::now();
-    fprintf(stderr, "qsmd5 trace: %zu chunks: classify %.2f ms, sort %.2f ms, plan %.2f ms, "
+    fprintf(stderr, "qsmd5 trace: %zu chunks: classify %.2f ms, sort %.2f ms, plan %.2f ms "
+            "(staging plan %.2f, copy runs + gather rows %.2f, descriptors %.2f), "
             "enqueue+run %.2f ms\n", n, ms(t0, t_classified), ms(t_classified, t_sorted),
-            ms(t_sorted, t_planned), ms(t_planned, t_end));
+            ms(t_sorted, t_planned), ms(t_sorted, t_hostplan), ms(t_hostplan, t_runs),
+            ms(t_runs, t_planned), ms(t_planned, t_end));
     fprintf(stderr, "qsmd5 trace: %zu slices, column width %llu, %zu groups, %zu regions, "
             "%zu gathered rows\n", slices.size(), (unsigned long long)(W == kNoColumns ? 0 : W),
             groups.size(), nregions, ngather);
