@@ -55,9 +55,11 @@ def _map_at(addr, size):
 
 def _pageable_near(pinned, above):
     """A pageable mapping next to `pinned` with >= GAP unmapped bytes between."""
-    # HIP packs its own mappings around pinned buffers: search up to ~16 GiB away
-    for k in list(range(1, 512)) + [512 * j for j in range(2, 16)]:
-        off = SIZE + GAP * k
+    # HIP packs its own mappings around pinned buffers and may reserve a large
+    # range next to them: search densely up to 1 GiB away, then at doubling
+    # distances up to 512 GiB (a 2-D run needs a stride below 2^40)
+    offs = [SIZE + GAP * k for k in range(1, 512)] + [1 << j for j in range(31, 40)]
+    for off in offs:
         addr = pinned + off if above else pinned - off
         addr &= ~(mmap.PAGESIZE - 1)
         if addr <= 0:
