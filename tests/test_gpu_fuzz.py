@@ -6,7 +6,13 @@ duplicates, and the runtime's knobs drawn per batch:
 - QSMD5_COLUMN_BYTES: automatic, whole chunks, or a forced width;
 - QSMD5_KERNEL: automatic or forced;
 - QSMD5_MAPS_AFTER: VMA classification on early or off;
-- QSMD5_FLAG_HOST: when every chunk is host memory.
+- QSMD5_FLAG_HOST: when every chunk is host memory;
+- QSMD5_GATHER / QSMD5_GATHER_GROUPS: the gather kernel for lone pinned rows,
+  on, off, or with 1..16 workgroups;
+- QSMD5_PC_LANES and QSMD5_LOAD_NT: lanes per latency-kernel workgroup and nt
+  producer loads.
+Host chunks come from two separate pinned pools, a pageable pool and a
+pageable pool registered with qsmd5_register_host.
 This drives the paths the fixed tests pin one at a time: the inline small-batch
 path, single- and multi-slice staging, column kernels, the classifier's range
 caches and 2-D copy runs.
@@ -29,6 +35,8 @@ POOL = 24 << 20
 N_BATCH = int(os.environ.get("QSMD5_FUZZ_SEEDS", "64"))
 N_STREAM = max(16, N_BATCH // 4)
 EDGES = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 4095, 4096, 4097]
+KNOBS = ("QSMD5_COLUMN_BYTES", "QSMD5_KERNEL", "QSMD5_MAPS_AFTER", "QSMD5_GATHER",
+         "QSMD5_GATHER_GROUPS", "QSMD5_PC_LANES", "QSMD5_LOAD_NT")
 
 
 @pytest.fixture(scope="module")
@@ -42,10 +50,17 @@ def pools():
     pp = qsmd5.alloc_pinned(POOL)
     pinned = np.ctypeslib.as_array((ctypes.c_uint8 * POOL).from_address(pp))
     pinned[:] = host
+    pp2 = qsmd5.alloc_pinned(POOL)
+    pinned2 = np.ctypeslib.as_array((ctypes.c_uint8 * POOL).from_address(pp2))
+    pinned2[:] = host
+    reg = host.copy()
+    qsmd5.register_host(reg.ctypes.data, POOL)
     torch.cuda.synchronize()
-    yield {"host": host, "dev": dev, "pinned": pinned}
+    yield {"host": host, "dev": dev, "pinned": pinned, "pinned2": pinned2, "reg": reg}
+    qsmd5.unregister_host(reg.ctypes.data)
     qsmd5.free_pinned(pp)
-    for k in ("QSMD5_COLUMN_BYTES", "QSMD5_KERNEL", "QSMD5_MAPS_AFTER"):
+    qsmd5.free_pinned(pp2)
+    for k in KNOBS:
         os.environ.pop(k, None)
 
 
@@ -59,7 +74,9 @@ def _length(rng):
 def test_random_batches(pools, seed):
     rng = random.Random(seed)
     n = rng.choice([1, 2, 3, 17, 64, 65, 200, 300])
-    kinds = rng.choice([["dev"], ["pinned"], ["host"], ["pinned", "host"], ["dev", "pinned", "host"]])
+    kinds = rng.choice([["dev"], ["pinned"], ["host"], ["pinned", "host"], ["dev", "pinned", "host"],
+                        ["pinned", "pinned2"], ["pinned", "pinned2", "reg"], ["reg", "host"],
+                        ["dev", "pinned2", "reg", "host"]])
     chunks, refs = [], []
     for _ in range(n):
         L = _length(rng)
@@ -78,6 +95,10 @@ def test_random_batches(pools, seed):
         "QSMD5_COLUMN_BYTES": rng.choice([None, None, "0", "1024", "4160", str(256 << 10)]),
         "QSMD5_KERNEL": rng.choice([None, None, "pc", "pc2", "v1", "coal"]),
         "QSMD5_MAPS_AFTER": rng.choice([None, "1", "100000000"]),
+        "QSMD5_GATHER": rng.choice([None, None, "0"]),
+        "QSMD5_GATHER_GROUPS": rng.choice([None, "1", "3", "16"]),
+        "QSMD5_PC_LANES": rng.choice([None, None, "16", "32", "48"]),
+        "QSMD5_LOAD_NT": rng.choice([None, None, "1"]),
     }
     for k, v in env.items():
         if v is None:
