@@ -270,53 +270,6 @@ __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*rin
   }
 }
 
-__device__ __forceinline__ void pc_read_slot(u32x4 (&dst)[16], const u32x4 (*ring)[16][64],
-                                             uint32_t slot, uint32_t lane) {
-#pragma unroll
-  for (int g = 0; g < 16; ++g) dst[g] = ring[slot][g][lane];
-}
-
-// chain_phase with the phase barrier inside the last block (kEarly): after the
-// wait for block kHalf-1's operands the chain meets the producer's barrier, so
-// the producer has written the next phase and this half is fully in registers;
-// it then reads the next phase's first block (into `a`) while block kHalf-1
-// compresses.  Without this, each phase starts with 16 exposed ds_read_b128
-// queued behind the producer's 64 ring writes.  `a` holds block 0's operands
-// on entry; kHalf must be even so block kHalf's operands land in `a` again.
-template <bool kAllLive, int kHalf>
-__device__ __forceinline__ void chain_phase_early(uint32_t (&st)[4], const u32x4 (*ring)[16][64],
-                                                  uint32_t s0, uint32_t s_next, bool more,
-                                                  uint32_t lane, uint32_t blk0, uint32_t nblk,
-                                                  u32x4 (&a)[16]) {
-  static_assert(kHalf % 2 == 0, "next phase's block 0 must land in a");
-  u32x4 b[16];
-  auto compress_slot = [&](const u32x4 (&src)[16]) {
-    uint32_t mk[64];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      mk[4 * g + 0] = src[g].x;
-      mk[4 * g + 1] = src[g].y;
-      mk[4 * g + 2] = src[g].z;
-      mk[4 * g + 3] = src[g].w;
-    }
-    md5_compress_mk(st, mk);
-  };
-#pragma unroll
-  for (int h = 0; h < kHalf; ++h) {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
-    asm volatile("" ::: "memory");  // keep each block's reads here (no IR-level hoisting)
-    if (h + 1 < kHalf) {
-      pc_read_slot((h & 1) ? a : b, ring, s0 + h + 1, lane);
-    } else {
-      lds_barrier();
-      (void)more;  // the last phase reads a stale half: harmless, never used
-      pc_read_slot(a, ring, s_next, lane);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (kAllLive || blk0 + (uint32_t)h < nblk) compress_slot((h & 1) ? b : a);
-  }
-}
 
 }  // namespace qsmd5
 
@@ -434,8 +387,7 @@ constexpr uint32_t kSkewMinBlocks = 1u << 19;
 // launch by the host, qsmd5_runtime.cpp load_nt_for).
 // kTrace (ubench only): the chain wave's lane 0 stamps s_memtime and
 // s_memrealtime every 4096 phases into trace[workgroup][2 * (p / 4096) + {0,1}].
-template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false,
-          bool kEarly = false>
+template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
                                         uint32_t* __restrict__ digests, uint64_t col_off,
@@ -539,21 +491,7 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     st[3] = s4.w;
   }
   lds_barrier();
-  if constexpr (kEarly) {
-    u32x4 a[16];
-    pc_read_slot(a, ring, 0, lane);  // phase 0, block 0 (harmless if phases == 0)
-    for (uint32_t p = 0; p < phases; ++p) {
-      const uint32_t s0 = (p & 1u) * kHalf;
-      const uint32_t sn = ((p + 1u) & 1u) * kHalf;
-      if (p >= live_lo && p < live_hi)
-        chain_phase_early<true, kHalf>(st, ring, s0, sn, p + 1 < phases, lane, p * kHalf - delta,
-                                       nblk, a);
-      else
-        chain_phase_early<false, kHalf>(st, ring, s0, sn, p + 1 < phases, lane, p * kHalf - delta,
-                                        nblk, a);
-    }
-  }
-  for (uint32_t p = 0; !kEarly && p < phases; ++p) {
+  for (uint32_t p = 0; p < phases; ++p) {
     if constexpr (kTrace) {
       if (lane == 0 && (p & 4095u) == 0u) {
         uint64_t* tr = trace + (uint64_t)blockIdx.x * 1024u + 2u * (p >> 12);
