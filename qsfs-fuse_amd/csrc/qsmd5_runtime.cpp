@@ -30,6 +30,7 @@
 #include <condition_variable>
 #include <map>
 #include <mutex>
+#include <memory>
 #include <new>
 #include <numeric>
 #include <string>
@@ -1302,8 +1303,10 @@ bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
 }
 
 // The CPU backend: every chunk on up to cpu_threads() host threads (longest
-// first, taken from a shared counter).  Device-resident chunks are first
-// copied to host memory; that needs a working HIP context.
+// first, taken from a shared counter).  A device-resident chunk is read through
+// the thread's own 8 MiB host buffer, piece by piece, so a fallback over a large
+// device batch holds at most 8 MiB per thread of host memory; that needs a
+// working HIP context.
 int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
   std::vector<uint64_t> len(n);
   uint64_t total = 0;
@@ -1316,9 +1319,7 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   }
   // Device memory cannot be read by a host core: find it (only where HIP has
   // devices at all, and not when the caller vouches for host memory).
-  std::vector<const uint8_t*> src(n);
-  for (size_t i = 0; i < n; ++i) src[i] = static_cast<const uint8_t*>(chunks[i].ptr);
-  std::vector<std::vector<uint8_t>> copies;
+  std::vector<uint8_t> on_dev(n, 0);
   if (!(flags & QSMD5_FLAG_HOST) && qsmd5_device_count() > 0) {
     Classifier cls(flags, n);
     for (size_t i = 0; i < n; ++i) {
@@ -1326,20 +1327,38 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
       if (!len[i] || cls(chunks[i].ptr, &owner) != kDeviceMem) continue;
       if (g_gpu_lost.load())
         return fail(-EIO, "qsmd5: the GPU context is lost; a device-resident chunk cannot be read");
-      copies.emplace_back(len[i]);
-      hipError_t e = hipMemcpy(copies.back().data(), chunks[i].ptr, len[i], hipMemcpyDeviceToHost);
-      if (e != hipSuccess) return hip_fail(e, "qsmd5 CPU backend: hipMemcpy D2H of a device chunk");
-      src[i] = copies.back().data();
+      on_dev[i] = 1;
     }
   }
   std::vector<uint32_t> order(n);
   std::iota(order.begin(), order.end(), 0u);
   std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len[a] > len[b]; });
   std::atomic<size_t> next{0};
-  auto work = [&] {
-    for (size_t k; (k = next.fetch_add(1)) < n;) {
+  std::atomic<int> hip_err{(int)hipSuccess};
+  auto set_err = [&](hipError_t e) {
+    int ok = (int)hipSuccess;
+    hip_err.compare_exchange_strong(ok, (int)e);
+  };
+  auto work = [&]() noexcept {
+    std::unique_ptr<uint8_t[]> bounce;
+    for (size_t k; (k = next.fetch_add(1)) < n && hip_err.load() == (int)hipSuccess;) {
       const uint32_t i = order[k];
-      qsmd5::cpu::md5(src[i], len[i], digests[i]);
+      const uint8_t* p = static_cast<const uint8_t*>(chunks[i].ptr);
+      if (!on_dev[i]) {
+        qsmd5::cpu::md5(p, len[i], digests[i]);
+        continue;
+      }
+      constexpr uint64_t kPiece = 8ull << 20;
+      if (!bounce) bounce.reset(new (std::nothrow) uint8_t[kPiece]);
+      if (!bounce) return set_err(hipErrorOutOfMemory);
+      qsmd5::cpu::Ctx c;
+      for (uint64_t off = 0; off < len[i]; off += kPiece) {
+        const uint64_t m = std::min(kPiece, len[i] - off);
+        const hipError_t e = hipMemcpy(bounce.get(), p + off, m, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return set_err(e);
+        c.update(bounce.get(), m);
+      }
+      c.final(digests[i]);
     }
   };
   // Threads only where they pay (a thread start costs ~20-50 us): >= 1 MiB
@@ -1355,6 +1374,9 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   }
   work();
   for (auto& t : th) t.join();
+  if (hip_err.load() != (int)hipSuccess)
+    return hip_fail((hipError_t)hip_err.load(), "qsmd5 CPU backend: reading a device chunk (8 MiB "
+                                                "host buffer or hipMemcpy D2H)");
   return 0;
 }
 

@@ -83,12 +83,18 @@ def test_lone_part_goes_to_the_cpu_and_beats_the_reference(auto):
 
 def test_injected_gpu_fault_falls_back_with_identical_digests(auto, monkeypatch):
     host_bufs, host = _batch(48, MiB)
-    dev = torch.empty(16 * MiB, dtype=torch.uint8, device="cuda")
+    # 16 device chunks of 1 MiB plus one of 19 MiB + 13 B, which the CPU backend
+    # reads back in 8 MiB pieces
+    big = 19 * MiB + 13
+    dev = torch.empty(16 * MiB + big, dtype=torch.uint8, device="cuda")
     qsmd5.synth_fill_lcg(dev.data_ptr(), MiB, MiB, 900, 16, torch.cuda.current_stream().cuda_stream)
+    qsmd5.synth_fill_lcg(dev.data_ptr() + 16 * MiB, big, big, 916, 1,
+                         torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    dchunks = [(dev.data_ptr() + i * MiB, MiB) for i in range(16)]
+    dchunks = [(dev.data_ptr() + i * MiB, MiB) for i in range(16)] + [(dev.data_ptr() + 16 * MiB + 0, big)]
     dhost = dev.cpu().numpy()
-    want = md5_many(host) + md5_many([(dhost.ctypes.data + i * MiB, MiB) for i in range(16)])
+    want = md5_many(host) + md5_many([(dhost.ctypes.data + i * MiB, MiB) for i in range(16)]
+                                     + [(dhost.ctypes.data + 16 * MiB, big)])
     monkeypatch.setenv("QSMD5_INJECT_GPU_FAULT", "1")
     s0 = qsmd5.stats()
     assert qsmd5.hash_batch(host + dchunks) == want  # device chunks come back by D2H
