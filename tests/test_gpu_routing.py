@@ -81,20 +81,34 @@ def test_lone_part_goes_to_the_cpu_and_beats_the_reference(auto):
     assert ours <= ref * 1.05
 
 
+def test_cpu_backend_reads_long_device_chunks_in_pieces(auto):
+    """The CPU backend reads a device chunk back through an 8 MiB host buffer:
+    chunks of 8 MiB - 1 .. 19 MiB + 13 B, ragged ends, against the oracle."""
+    lens = [8 * MiB - 1, 8 * MiB, 8 * MiB + 1, 19 * MiB + 13]
+    offs = [0]
+    for L in lens[:-1]:
+        offs.append(offs[-1] + L + 3)  # odd starts too
+    dev = torch.empty(offs[-1] + lens[-1], dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for k, (o, L) in enumerate(zip(offs, lens)):
+        qsmd5.synth_fill_lcg(dev.data_ptr() + o, L, L, 950 + k, 1, s)
+    torch.cuda.synchronize()
+    dhost = dev.cpu().numpy()
+    want = md5_many([(dhost.ctypes.data + o, L) for o, L in zip(offs, lens)])
+    got = qsmd5.hash_batch([(dev.data_ptr() + o, L) for o, L in zip(offs, lens)],
+                           flags=qsmd5.FLAG_CPU_ONLY)
+    assert got == want
+    assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
+
+
 def test_injected_gpu_fault_falls_back_with_identical_digests(auto, monkeypatch):
     host_bufs, host = _batch(48, MiB)
-    # 16 device chunks of 1 MiB plus one of 19 MiB + 13 B, which the CPU backend
-    # reads back in 8 MiB pieces
-    big = 19 * MiB + 13
-    dev = torch.empty(16 * MiB + big, dtype=torch.uint8, device="cuda")
+    dev = torch.empty(16 * MiB, dtype=torch.uint8, device="cuda")
     qsmd5.synth_fill_lcg(dev.data_ptr(), MiB, MiB, 900, 16, torch.cuda.current_stream().cuda_stream)
-    qsmd5.synth_fill_lcg(dev.data_ptr() + 16 * MiB, big, big, 916, 1,
-                         torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
-    dchunks = [(dev.data_ptr() + i * MiB, MiB) for i in range(16)] + [(dev.data_ptr() + 16 * MiB + 0, big)]
+    dchunks = [(dev.data_ptr() + i * MiB, MiB) for i in range(16)]
     dhost = dev.cpu().numpy()
-    want = md5_many(host) + md5_many([(dhost.ctypes.data + i * MiB, MiB) for i in range(16)]
-                                     + [(dhost.ctypes.data + 16 * MiB, big)])
+    want = md5_many(host) + md5_many([(dhost.ctypes.data + i * MiB, MiB) for i in range(16)])
     monkeypatch.setenv("QSMD5_INJECT_GPU_FAULT", "1")
     s0 = qsmd5.stats()
     assert qsmd5.hash_batch(host + dchunks) == want  # device chunks come back by D2H
