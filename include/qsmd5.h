@@ -225,15 +225,22 @@ QSMD5_API int qsmd5_verify_etag(const void* ptr, uint64_t len, const char* etag)
 
 /* Backend of the calling thread's last hashing call (hash_batch[_ex],
  * hash_one, hash_parts, verify_etag): QSMD5_BACKEND_GPU, QSMD5_BACKEND_CPU,
- * or 0 before the first call. */
+ * QSMD5_BACKEND_SPLIT (both at once: see qsmd5_route), or 0 before the first
+ * call. */
 #define QSMD5_BACKEND_GPU 1
 #define QSMD5_BACKEND_CPU 2
+#define QSMD5_BACKEND_SPLIT 3
 QSMD5_API int qsmd5_last_backend(void);
 
 /* The backend QSMD5_BACKEND=auto picks for this batch while the GPU is
- * healthy (host-only, needs no GPU): QSMD5_BACKEND_CPU when the CPU's
- * estimated time is the lower (QSMD5_CPU_THREADS threads, default 4, at
- * QSMD5_CPU_GIBS GiB/s each, default 0.7), else QSMD5_BACKEND_GPU. */
+ * healthy: QSMD5_BACKEND_CPU when the CPU's estimated time is the lower
+ * (QSMD5_CPU_THREADS threads, default 4, at QSMD5_CPU_GIBS GiB/s each,
+ * default 0.7); QSMD5_BACKEND_SPLIT when the batch is ragged enough that
+ * handing its longest host chunks to the CPU threads while the GPU hashes the
+ * rest cuts the estimate by >= 10% (a device chunk in the CPU share is read
+ * back to the host first; QSMD5_SPLIT=0 turns splitting off); else
+ * QSMD5_BACKEND_GPU.  A split call counts once in both gpu_batches and
+ * cpu_batches of qsmd5_stats. */
 QSMD5_API int qsmd5_route(const qsmd5_chunk* chunks, size_t n, int flags);
 
 /* Process-wide backend counters since load. */

@@ -1249,6 +1249,7 @@ int guarded(F&& f) {
 constexpr double kGpuChainGiBs = 0.119;
 constexpr double kLinkGiBs = 53.7;
 constexpr double kGpuCallMs = 0.03;
+constexpr double kD2HGiBs = 10.0;  // device chunk read back by the CPU backend (8 MiB pieces)
 
 enum Backend { kAuto = 0, kGpu = 1, kCpu = 2 };
 
@@ -1286,20 +1287,85 @@ double cpu_gibs_per_thread() {
   return v > 0 ? v : 0.7;
 }
 
+// Estimated wall time (ms) of a batch whose longest chunk is `longest` bytes
+// and whose chunks total `total` bytes, on each backend (see above).
+double gpu_est_ms(uint64_t longest, uint64_t total) {
+  const double GiB = 1073741824.0;
+  return kGpuCallMs + 1e3 * ((double)longest / kGpuChainGiBs + (double)total / kLinkGiBs) / GiB;
+}
+double cpu_est_ms(uint64_t longest, uint64_t total) {
+  const double GiB = 1073741824.0;
+  const double T = (double)cpu_threads(), rc = cpu_gibs_per_thread();
+  return 1e3 * std::max((double)longest / rc, (double)total / (T * rc)) / GiB;
+}
+
+uint64_t routed_len(const qsmd5_chunk& c, int flags) {
+  return (flags & QSMD5_FLAG_REF_TRUNCATE32) ? (c.len & 0xffffffffull) : c.len;
+}
+
 // True when the CPU is expected to finish this batch first (see above).
 bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
   uint64_t total = 0, longest = 0;
   for (size_t i = 0; i < n; ++i) {
-    uint64_t L = chunks[i].len;
-    if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;
+    const uint64_t L = routed_len(chunks[i], flags);
     total += L;
     longest = std::max(longest, L);
   }
-  const double GiB = 1073741824.0;
-  const double T = (double)cpu_threads(), rc = cpu_gibs_per_thread();
-  const double cpu_ms = 1e3 * std::max((double)longest / rc, (double)total / (T * rc)) / GiB;
-  const double gpu_ms = kGpuCallMs + 1e3 * ((double)longest / kGpuChainGiBs + (double)total / kLinkGiBs) / GiB;
-  return cpu_ms < gpu_ms;
+  return cpu_est_ms(longest, total) < gpu_est_ms(longest, total);
+}
+
+// Ragged batches (qsfs -b sweeps, a file's parts plus small files): the GPU's
+// time is its longest chain, which a host core runs ~6x faster.  So the
+// longest host chunks go to the CPU threads while the GPU hashes the rest,
+// when that cuts the estimated time by at least 10% (QSMD5_SPLIT=0: never).
+// E.g. BASELINE config 4 (659 chunks, 8 KiB-64 MiB): the GPU alone needs one
+// 64 MiB chain, ~0.53 s.  A device-resident chunk can go too: the CPU share
+// then pays its copy to the host (kD2HGiBs, the CPU backend's 8 MiB pieces),
+// ~5 ms for 64 MiB against the ~0.45 s its chain takes on the GPU.  Returns
+// the chunks for the CPU, longest first, or an empty list.
+std::vector<uint32_t> plan_split(const qsmd5_chunk* chunks, size_t n, int flags) {
+  std::vector<uint32_t> none;
+  if (n < 2 || !env_u64("QSMD5_SPLIT", 1)) return none;
+  uint64_t total = 0, longest = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t L = routed_len(chunks[i], flags);
+    total += L;
+    longest = std::max(longest, L);
+  }
+  const double gpu_all = gpu_est_ms(longest, total);
+  // only where one chain, not the link, sets the GPU's time
+  const double chain_ms = 1e3 * (double)longest / kGpuChainGiBs / 1073741824.0;
+  if (chain_ms < 0.5 * gpu_all) return none;
+  const size_t K = std::min<size_t>(n - 1, std::max<size_t>(64, 64 * cpu_threads()));
+  std::vector<uint32_t> idx(n);
+  std::iota(idx.begin(), idx.end(), 0u);
+  auto longer = [&](uint32_t a, uint32_t b) {
+    const uint64_t la = routed_len(chunks[a], flags), lb = routed_len(chunks[b], flags);
+    return la != lb ? la > lb : a < b;
+  };
+  std::partial_sort(idx.begin(), idx.begin() + (K + 1), idx.end(), longer);
+  const bool classify_ptrs = !(flags & QSMD5_FLAG_HOST) && qsmd5_device_count() > 0;
+  std::unique_ptr<Classifier> cls(classify_ptrs ? new Classifier(flags, K) : nullptr);
+  double best = gpu_all;
+  size_t best_k = 0;
+  uint64_t cpu_bytes = 0, d2h_bytes = 0;
+  for (size_t k = 1; k <= K; ++k) {
+    const uint32_t i = idx[k - 1];
+    const uint64_t L = routed_len(chunks[i], flags);
+    int owner = -1;
+    if (cls && L && (*cls)(chunks[i].ptr, &owner) == kDeviceMem) d2h_bytes += L;
+    cpu_bytes += L;
+    const double copy_ms = 1e3 * (double)d2h_bytes / kD2HGiBs / 1073741824.0;
+    const double t = std::max(cpu_est_ms(routed_len(chunks[idx[0]], flags), cpu_bytes) + copy_ms,
+                              gpu_est_ms(routed_len(chunks[idx[k]], flags), total - cpu_bytes));
+    if (t < best) {
+      best = t;
+      best_k = k;
+    }
+  }
+  if (best_k == 0 || best > 0.9 * gpu_all) return none;
+  idx.resize(best_k);
+  return idx;
 }
 
 // The CPU backend: every chunk on up to cpu_threads() host threads (longest
@@ -1408,6 +1474,87 @@ void note_gpu_failure(int rc, bool injected_sticky) {
             "process to use the GPU again\n", why.c_str());
 }
 
+// One GPU attempt, with the test-only fault injection (QSMD5_INJECT_GPU_FAULT:
+// "1" fails every GPU batch as a HIP error would, "sticky" also marks the
+// context lost).
+int gpu_attempt(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int gflags,
+                bool* sticky) {
+  *sticky = false;
+  int rc = ensure_init();
+  if (rc) return rc;
+  const char* inj = getenv("QSMD5_INJECT_GPU_FAULT");
+  if (inj && *inj && strcmp(inj, "0")) {
+    *sticky = !strcmp(inj, "sticky");
+    return fail(-EIO, "qsmd5: injected GPU fault (QSMD5_INJECT_GPU_FAULT)");
+  }
+  return group_commit(chunks, n, digests, gflags);
+}
+
+// plan_split's batch: the CPU chunks on the CPU backend's threads, started
+// first, while this thread runs the rest through the GPU path.  A GPU failure
+// falls back to the CPU for the GPU's share (auto mode only reaches here).
+int run_split(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int gflags,
+              const std::vector<uint32_t>& to_cpu) {
+  std::vector<uint8_t> on_cpu(n, 0);
+  for (uint32_t i : to_cpu) on_cpu[i] = 1;
+  std::vector<qsmd5_chunk> cc, gc;
+  std::vector<uint32_t> cmap, gmap;
+  cc.reserve(to_cpu.size());
+  gc.reserve(n - to_cpu.size());
+  for (size_t i = 0; i < n; ++i) {
+    (on_cpu[i] ? cc : gc).push_back(chunks[i]);
+    (on_cpu[i] ? cmap : gmap).push_back((uint32_t)i);
+  }
+  std::vector<uint8_t> cd(16 * cc.size()), gd(16 * gc.size());
+  auto* cdig = reinterpret_cast<uint8_t(*)[16]>(cd.data());
+  auto* gdig = reinterpret_cast<uint8_t(*)[16]>(gd.data());
+  int rc_cpu = 0;
+  std::string cpu_err;
+  auto cpu_side = [&]() noexcept {
+    try {
+      rc_cpu = cpu_batch(cc.data(), cc.size(), cdig, gflags);
+    } catch (...) {
+      rc_cpu = fail(-ENOMEM, "qsmd5: CPU share of a split batch failed");
+    }
+    if (rc_cpu) cpu_err = t_last_error;
+  };
+  log_call("gpu+cpu", "split", n, chunks);
+  std::thread th;
+  bool threaded = true;
+  try {
+    th = std::thread(cpu_side);
+  } catch (...) {
+    threaded = false;  // no thread: the CPU share runs after the GPU's
+  }
+  bool sticky = false;
+  int rc = gpu_attempt(gc.data(), gc.size(), gdig, gflags, &sticky);
+  if (threaded) th.join(); else cpu_side();
+  bool gpu_failed = false;
+  if (rc) {
+    if (rc == -EINVAL) return rc;
+    note_gpu_failure(rc, sticky);
+    const std::string gpu_err = t_last_error;
+    if (int rc2 = cpu_batch(gc.data(), gc.size(), gdig, gflags))
+      return fail(rc2, t_last_error + " (after GPU failure: " + gpu_err + ")");
+    g_fallbacks.fetch_add(1);
+    gpu_failed = true;
+  }
+  if (rc_cpu) return fail(rc_cpu, cpu_err);
+  for (size_t k = 0; k < cc.size(); ++k) memcpy(digests[cmap[k]], cdig[k], 16);
+  for (size_t k = 0; k < gc.size(); ++k) memcpy(digests[gmap[k]], gdig[k], 16);
+  g_cpu_batches.fetch_add(1);
+  if (gpu_failed) {
+    g_cpu_chunks.fetch_add(n);
+    t_last_backend = QSMD5_BACKEND_CPU;
+  } else {
+    g_gpu_batches.fetch_add(1);
+    g_cpu_chunks.fetch_add(cc.size());
+    g_gpu_chunks.fetch_add(gc.size());
+    t_last_backend = QSMD5_BACKEND_SPLIT;
+  }
+  return 0;
+}
+
 int hash_routed(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
   Backend b = kAuto;
   if (int rc = requested_backend(flags, &b)) return rc;
@@ -1426,21 +1573,12 @@ int hash_routed(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
   if (b == kAuto) {
     if (g_gpu_lost.load()) return on_cpu("gpu-lost");
     if (cpu_is_faster(chunks, n, gflags)) return on_cpu("size");
+    const std::vector<uint32_t> to_cpu = plan_split(chunks, n, gflags);
+    if (!to_cpu.empty()) return run_split(chunks, n, digests, gflags, to_cpu);
   }
   log_call("gpu", b == kGpu ? "forced" : "size", n, chunks);
-  int rc = ensure_init();
   bool sticky = false;
-  if (rc == 0) {
-    // QSMD5_INJECT_GPU_FAULT (tests): "1" fails every GPU batch as a HIP error
-    // would, "sticky" also marks the context lost.
-    const char* inj = getenv("QSMD5_INJECT_GPU_FAULT");
-    if (inj && *inj && strcmp(inj, "0")) {
-      sticky = !strcmp(inj, "sticky");
-      rc = fail(-EIO, "qsmd5: injected GPU fault (QSMD5_INJECT_GPU_FAULT)");
-    } else {
-      rc = group_commit(chunks, n, digests, gflags);
-    }
-  }
+  int rc = gpu_attempt(chunks, n, digests, gflags, &sticky);
   if (rc == 0) {
     t_last_backend = QSMD5_BACKEND_GPU;
     g_gpu_batches.fetch_add(1);
@@ -1734,7 +1872,10 @@ int qsmd5_last_backend(void) { return t_last_backend; }
 
 int qsmd5_route(const qsmd5_chunk* chunks, size_t n, int flags) {
   if (n && !chunks) return fail(-EINVAL, "qsmd5: NULL chunks");
-  return cpu_is_faster(chunks, n, flags) ? QSMD5_BACKEND_CPU : QSMD5_BACKEND_GPU;
+  return guarded([&] {
+    if (cpu_is_faster(chunks, n, flags)) return QSMD5_BACKEND_CPU;
+    return plan_split(chunks, n, flags).empty() ? QSMD5_BACKEND_GPU : QSMD5_BACKEND_SPLIT;
+  });
 }
 
 int qsmd5_get_stats(qsmd5_stats* out) {

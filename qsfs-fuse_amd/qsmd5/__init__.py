@@ -24,7 +24,7 @@ __all__ = [
     "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
     "alloc_pinned", "free_pinned", "register_host", "unregister_host", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
     "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST", "FLAG_GPU_ONLY",
-    "FLAG_CPU_ONLY", "stats", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU",
+    "FLAG_CPU_ONLY", "stats", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU", "BACKEND_SPLIT",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -168,6 +168,7 @@ FLAG_GPU_ONLY = 8  # gfx950 kernels only: no CPU routing or fallback
 FLAG_CPU_ONLY = 16  # the library's CPU MD5 only
 BACKEND_GPU = 1
 BACKEND_CPU = 2
+BACKEND_SPLIT = 3  # both at once: the longest host chunks on the CPU, the rest on the GPU
 
 
 def stats():
@@ -178,18 +179,20 @@ def stats():
 
 
 def route(lengths, flags=0):
-    """Backend (BACKEND_CPU / BACKEND_GPU) that QSMD5_BACKEND=auto picks for a
-    batch of chunks of these lengths (host logic; no data is read)."""
+    """Backend (BACKEND_CPU / BACKEND_GPU / BACKEND_SPLIT) that
+    QSMD5_BACKEND=auto picks for a batch of host chunks of these lengths (host
+    logic; no data is read, the pointers are placeholders)."""
     n = len(lengths)
     arr = (qsmd5_chunk * max(n, 1))()
     for i, L in enumerate(lengths):
         arr[i].ptr = 1 if L else 0
         arr[i].len = L
-    return lib().qsmd5_route(arr, n, flags)
+    return lib().qsmd5_route(arr, n, flags | FLAG_HOST)
 
 
 def last_backend():
-    """BACKEND_GPU / BACKEND_CPU of this thread's last hashing call (0: none)."""
+    """BACKEND_GPU / BACKEND_CPU / BACKEND_SPLIT of this thread's last hashing
+    call (0: none)."""
     return lib().qsmd5_last_backend()
 
 

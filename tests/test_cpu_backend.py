@@ -16,13 +16,14 @@ QSMD5_BACKEND=cpu/auto; without a GPU, auto mode takes the fallback path.
 import ctypes
 import errno
 import os
+import random
 import subprocess
 
 import pytest
 
 import qsmd5
 from conftest import ROOT
-from oracle_util import lcg_bytes
+from oracle_util import lcg_bytes, md5_many
 
 CPU = qsmd5.FLAG_CPU_ONLY
 
@@ -155,6 +156,48 @@ def test_routing_rule(monkeypatch):
     monkeypatch.delenv("QSMD5_CPU_THREADS")
     seq = [qsmd5.route([MiB] * n) for n in range(1, 200)]
     assert seq == sorted(seq, key=lambda b: b == G)
+
+
+def _config4_lengths():
+    """BASELINE config 4's shape: 659 chunks, log-uniform 8 KiB-64 MiB."""
+    rng = random.Random(7)
+    return [int(2 ** rng.uniform(13, 26)) for _ in range(659)]
+
+
+def test_split_routing_rule(monkeypatch):
+    """Ragged batches split: the longest host chunks go to the CPU threads while
+    the GPU hashes the rest (qsmd5_route -> BACKEND_SPLIT).  Equal parts and
+    many small objects never split; QSMD5_SPLIT=0 turns it off."""
+    monkeypatch.delenv("QSMD5_CPU_THREADS", raising=False)
+    monkeypatch.delenv("QSMD5_CPU_GIBS", raising=False)
+    monkeypatch.delenv("QSMD5_SPLIT", raising=False)
+    MiB = 1 << 20
+    S, G = qsmd5.BACKEND_SPLIT, qsmd5.BACKEND_GPU
+    lens = _config4_lengths()
+    assert qsmd5.route(lens) == S
+    assert qsmd5.route([10 * MiB] * 512) == G
+    assert qsmd5.route([10 * MiB] * 512 + [64 * MiB]) == S  # one long straggler
+    assert qsmd5.route([1024] * (1 << 16) + [4096]) == G  # the link, not a chain, sets the time
+    monkeypatch.setenv("QSMD5_SPLIT", "0")
+    assert qsmd5.route(lens) == G
+    assert qsmd5.route([10 * MiB] * 512 + [64 * MiB]) == G
+
+
+def test_split_batch_digests_on_cpu_only_box(monkeypatch):
+    """Without a GPU a split batch still returns every digest (its GPU share
+    falls back to the CPU) and matches the oracle chunk by chunk."""
+    monkeypatch.setenv("QSMD5_BACKEND", "auto")
+    monkeypatch.setenv("QSMD5_CPU_THREADS", "1")  # a small batch that still favours the GPU
+    monkeypatch.delenv("QSMD5_SPLIT", raising=False)
+    MiB = 1 << 20
+    lens = [MiB + 7, 64, 0, MiB, 999] * 10 + [4 * MiB + 3, 3 * MiB]
+    assert qsmd5.route(lens) == qsmd5.BACKEND_SPLIT
+    bufs = [lcg_bytes(700 + i, L) for i, L in enumerate(lens)]
+    chunks = [(ctypes.addressof(b) if L else 0, L) for b, L in zip(bufs, lens)]
+    s0 = qsmd5.stats()
+    assert qsmd5.hash_batch(chunks) == md5_many(chunks)
+    assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
+    assert qsmd5.stats()["fallbacks"] == s0["fallbacks"] + 1
 
 
 def test_log_names_the_backend(tmp_path):

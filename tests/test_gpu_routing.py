@@ -178,3 +178,69 @@ def test_streaming_class_in_auto_mode_reads_device_pieces(auto):
         off += c
     assert off == L
     assert h.finalize().digest() == md5_many([(host.ctypes.data, L)])[0]
+
+
+def _ragged_host(seed=31):
+    """60 chunks of ~1-3 MiB and two of 16 MiB + a few bytes (host, pageable)."""
+    import random
+    rng = random.Random(seed)
+    lens = [MiB + rng.randrange(2 * MiB) for _ in range(60)] + [16 * MiB + 5, 16 * MiB + 77]
+    rng.shuffle(lens)
+    bufs = [lcg_bytes(seed * 1000 + i, L) for i, L in enumerate(lens)]
+    return lens, bufs, [(ctypes.addressof(b), L) for b, L in zip(bufs, lens)]
+
+
+def test_split_ragged_host_batch(auto, monkeypatch):
+    """A ragged batch splits: its two long chunks go to the CPU threads while
+    the GPU hashes the other 60; every digest equals the oracle's."""
+    monkeypatch.setenv("QSMD5_CPU_THREADS", "1")
+    lens, _bufs, chunks = _ragged_host()
+    assert qsmd5.route(lens) == qsmd5.BACKEND_SPLIT
+    s0 = qsmd5.stats()
+    assert qsmd5.hash_batch(chunks) == md5_many(chunks)
+    assert qsmd5.last_backend() == qsmd5.BACKEND_SPLIT
+    s1 = qsmd5.stats()
+    assert s1["gpu_batches"] == s0["gpu_batches"] + 1 and s1["cpu_batches"] == s0["cpu_batches"] + 1
+    took = s1["cpu_chunks"] - s0["cpu_chunks"]
+    assert 2 <= took < len(lens) and s1["gpu_chunks"] - s0["gpu_chunks"] == len(lens) - took
+    monkeypatch.setenv("QSMD5_SPLIT", "0")
+    assert qsmd5.hash_batch(chunks) == md5_many(chunks)
+    assert qsmd5.last_backend() == qsmd5.BACKEND_GPU
+
+
+def test_split_batch_gpu_fault_falls_back(auto, monkeypatch):
+    monkeypatch.setenv("QSMD5_CPU_THREADS", "1")
+    lens, _bufs, chunks = _ragged_host(seed=32)
+    monkeypatch.setenv("QSMD5_INJECT_GPU_FAULT", "1")
+    s0 = qsmd5.stats()
+    assert qsmd5.hash_batch(chunks) == md5_many(chunks)
+    assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
+    s1 = qsmd5.stats()
+    assert s1["fallbacks"] == s0["fallbacks"] + 1 and not s1["gpu_lost"]
+
+
+def test_split_config4_device_resident(auto, golden):
+    """BASELINE config 4 (659 device-resident chunks, 0 B-64 MiB) under auto
+    routing: the longest chunks are read back and hashed by the CPU threads
+    while the GPU runs the rest; all 659 digests equal the reference's."""
+    gr = golden("ragged.json")
+    lens = gr["lengths"]
+    offs, pos = [], 0
+    for L in lens:
+        offs.append(pos)
+        pos += (L + 255) & ~255
+    t = torch.empty(pos + 256, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        qsmd5.synth_fill_lcg(t.data_ptr() + o, 0, L, 7000 + i, 1, s)
+    torch.cuda.synchronize()
+    chunks = [(t.data_ptr() + o, L) for o, L in zip(offs, lens)]
+    t0 = time.perf_counter()
+    digs = qsmd5.hash_batch(chunks)
+    split_s = time.perf_counter() - t0
+    assert [d.hex() for d in digs] == gr["md5"]
+    assert qsmd5.last_backend() == qsmd5.BACKEND_SPLIT
+    t0 = time.perf_counter()
+    assert [d.hex() for d in qsmd5.hash_batch(chunks, flags=qsmd5.FLAG_GPU_ONLY)] == gr["md5"]
+    gpu_s = time.perf_counter() - t0
+    print("config 4 device-resident: split %.3f s, GPU only %.3f s" % (split_s, gpu_s))
