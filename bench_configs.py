@@ -253,6 +253,54 @@ def config4(reps):
                                            "synchronous qsmd5_hash_batch", "results": sweep})
 
 
+def config4_split(reps):
+    """Config 4 under QSMD5_BACKEND=auto, where a ragged batch splits: its
+    longest chunks go to the CPU threads (QSMD5_CPU_THREADS, default 4) while
+    the GPU hashes the rest.  Device-resident and pageable host-resident, each
+    against the same batch on the GPU alone (QSMD5_FLAG_GPU_ONLY)."""
+    import numpy as np
+    import torch
+    import qsmd5
+    gr = gold("ragged.json")
+    lens = gr["lengths"]
+    offs, pos = [], 0
+    for L in lens:
+        offs.append(pos)
+        pos += (L + 255) & ~255
+    t = torch.empty(pos + 256, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for i, (o, L) in enumerate(zip(offs, lens)):
+        qsmd5.synth_fill_lcg(t.data_ptr() + o, 0, L, 7000 + i, 1, s)
+    torch.cuda.synchronize()
+    host = t.cpu().numpy()
+    tot = sum(lens)
+    prev = os.environ.get("QSMD5_BACKEND")
+    os.environ["QSMD5_BACKEND"] = "auto"
+    try:
+        for where, base in (("device-resident", t.data_ptr()), ("pageable host", host.ctypes.data)):
+            chunks = [(base + o, L) for o, L in zip(offs, lens)]
+            res = {}
+            for mode, flags in (("split", 0), ("gpu_only", qsmd5.FLAG_GPU_ONLY)):
+                dt, digs = timed(lambda: qsmd5.hash_batch(chunks, flags=flags), reps)
+                res[mode] = (dt, [d.hex() for d in digs] == gr["md5"], qsmd5.last_backend())
+            emit({"config": "4-split", "workload": "ragged: %d chunks, 0 B..64 MiB = %.2f GiB, %s, "
+                                                   "QSMD5_BACKEND=auto" % (len(lens), tot / GiB, where),
+                  "cpu_threads": int(os.environ.get("QSMD5_CPU_THREADS", "4")),
+                  "split": {"GiBps": round(tot / GiB / res["split"][0], 3),
+                            "seconds": round(res["split"][0], 4),
+                            "backend": {1: "gpu", 2: "cpu", 3: "gpu+cpu"}.get(res["split"][2])},
+                  "gpu_only": {"GiBps": round(tot / GiB / res["gpu_only"][0], 3),
+                               "seconds": round(res["gpu_only"][0], 4)},
+                  "parity": "ok: %d/%d == reference golden, both modes" % (len(lens), len(lens))
+                  if res["split"][1] and res["gpu_only"][1] else "FAIL"})
+    finally:
+        if prev is None:
+            os.environ.pop("QSMD5_BACKEND", None)
+        else:
+            os.environ["QSMD5_BACKEND"] = prev
+    del t, host
+
+
 def config5(reps, n=10000):
     import torch
     import qsmd5
@@ -370,6 +418,8 @@ def main():
             config3_pageable(args.reps)
         elif c == "4":
             config4(args.reps)
+        elif c == "4split":
+            config4_split(args.reps)
         elif c == "5":
             config5(args.reps)
         elif c == "satpad":  # exact power-of-two strides vs the padded default
