@@ -83,7 +83,7 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
   }
   for (int r = 0; r < rounds; ++r) {
     uint8_t d[16];
-    switch ((t + r) % 4) {
+    switch ((t + r) % 5) {
       case 0: {  // one part, pageable, arbitrary offset and length
         const size_t off = next(s) % 61, len = next(s) % (max_len - 64) + 1;
         if ((rc = qsmd5_hash_one(buf.data() + off, len, d)) != 0) fail("hash_one", rc, t, r);
@@ -140,6 +140,22 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
         if ((rc = qsmd5_hash_one(p, len, d)) != 0) fail("hash_one(pinned)", rc, t, r);
         else check((const uint8_t*)p, len, d, "hash_one(pinned)", t, r);
         if ((rc = qsmd5_free_pinned(p)) != 0) fail("free_pinned", rc, t, r);
+        break;
+      }
+      case 4: {  // ragged: two long chunks among many short ones (split under auto routing)
+        const int n = 48;
+        std::vector<qsmd5_chunk> ch(n);
+        std::vector<uint8_t> dg(16 * n);
+        for (int i = 0; i < n; ++i) {
+          const size_t len = i < 2 ? max_len / 4 + next(s) % 4096 : (128u << 10) + next(s) % (128u << 10);
+          const size_t off = next(s) % (buf.size() - len + 1);
+          ch[(i * 7) % n].ptr = buf.data() + off;  // long ones land mid-batch
+          ch[(i * 7) % n].len = len;
+        }
+        if ((rc = qsmd5_hash_batch(ch.data(), n, (uint8_t(*)[16])dg.data())) != 0) fail("split batch", rc, t, r);
+        else
+          for (int i = 0; i < n; ++i)
+            check((const uint8_t*)ch[i].ptr, ch[i].len, dg.data() + 16 * i, "split batch", t, r);
         break;
       }
     }

@@ -28,7 +28,7 @@ REPORT_MARKERS = ("WARNING: ThreadSanitizer", "ERROR: AddressSanitizer", "runtim
 
 
 def _run(variant, devices, threads=6, rounds=12, max_len=3 << 20, extra=(), expect_clean=True,
-         backend="gpu", inject=None):
+         backend="gpu", inject=None, cpu_threads=None):
     exe = os.path.join(SAN, "race_stress_" + variant)
     if not os.path.exists(exe):
         pytest.fail("%s missing: run scripts/build_sanitized.sh (built by __graft_entry__.build())" % exe)
@@ -37,6 +37,13 @@ def _run(variant, devices, threads=6, rounds=12, max_len=3 << 20, extra=(), expe
     env.pop("QSMD5_INJECT_GPU_FAULT", None)
     if inject:
         env["QSMD5_INJECT_GPU_FAULT"] = inject
+    env.pop("QSMD5_CPU_THREADS", None)
+    env.pop("QSMD5_SPLIT", None)
+    env.pop("QSMD5_LOG", None)
+    if cpu_threads:
+        env["QSMD5_CPU_THREADS"] = str(cpu_threads)
+    if backend == "auto":
+        env["QSMD5_LOG"] = "1"  # the routing decisions, checked below
     env.pop("QSMD5_DEVICES", None)
     if devices:
         env["QSMD5_DEVICES"] = devices
@@ -57,7 +64,9 @@ def _run(variant, devices, threads=6, rounds=12, max_len=3 << 20, extra=(), expe
     assert out.returncode == 0, text[-6000:]
     assert "race_stress ok" in out.stdout, text[-3000:]
     sup = [ln for ln in out.stderr.splitlines() if "suppression" in ln.lower() or ln.strip().startswith(("race:", "called_from_lib:"))]
-    return out.stdout + "\n".join(sup)
+    routes = sorted({ln for ln in out.stderr.splitlines() if ln.startswith("qsmd5: backend=")
+                     for ln in [ln.split(" chunks=")[0]]})
+    return out.stdout + "\n".join(sup + routes)
 
 
 @pytest.mark.gpu
@@ -78,10 +87,15 @@ def test_race_stress_asan_ubsan(devices):
 @pytest.mark.parametrize("inject", [None, "1"], ids=["routed", "gpu_fault_fallback"])
 def test_race_stress_auto_backend(variant, inject):
     """QSMD5_BACKEND=auto: small calls and streams route to the library's CPU
-    MD5 (its helper threads included) while larger batches take the GPU; with
-    an injected GPU fault every GPU call falls back to the CPU.  Both under
-    the sanitizers, every digest against the oracle."""
-    print(_run(variant, "", backend="auto", inject=inject))
+    MD5 (its helper threads included) while larger batches take the GPU, and
+    ragged batches split between the two (one CPU thread, so that the
+    stress's small batches already favour the GPU); with an injected GPU fault
+    every GPU call falls back to the CPU.  Both under the sanitizers, every
+    digest against the oracle."""
+    out = _run(variant, "", backend="auto", inject=inject, cpu_threads=1)
+    print(out)
+    assert "backend=gpu+cpu reason=split" in out, out[-3000:]
+    assert "backend=cpu reason=size" in out, out[-3000:]
 
 
 @pytest.mark.gpu
