@@ -1526,6 +1526,12 @@ int run_split(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int g
   } catch (...) {
     threaded = false;  // no thread: the CPU share runs after the GPU's
   }
+  struct JoinOnExit {  // an exception from the GPU share must not leave `th` joinable
+    std::thread& t;
+    ~JoinOnExit() {
+      if (t.joinable()) t.join();
+    }
+  } join_on_exit{th};
   bool sticky = false;
   int rc = gpu_attempt(gc.data(), gc.size(), gdig, gflags, &sticky);
   if (threaded) th.join(); else cpu_side();
