@@ -33,8 +33,6 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include <type_traits>
-
 #include "md5_core.h"
 
 namespace qsmd5 {
@@ -272,47 +270,6 @@ __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*rin
   }
 }
 
-__device__ __forceinline__ void pc_read_slot(u32x4 (&dst)[16], const u32x4 (*ring)[16][64],
-                                             uint32_t slot, uint32_t lane) {
-#pragma unroll
-  for (int g = 0; g < 16; ++g) dst[g] = ring[slot][g][lane];
-}
-
-// One phase of the chain wave on a ring of kRing >= 3 halves, where the
-// producer writes two phases ahead: the next phase's first block is already
-// in LDS, so its operands are read during this phase's last block instead of
-// at the next phase's start.  Block j of the chunk uses register set j & 1;
-// kPar is the set this phase's first block uses (given, read ahead, on entry).
-template <bool kAllLive, int kHalf, int kPar>
-__device__ __forceinline__ void chain_phase_lead(uint32_t (&st)[4], const u32x4 (*ring)[16][64],
-                                                 uint32_t s0, uint32_t s_next, uint32_t lane,
-                                                 uint32_t blk0, uint32_t nblk, u32x4 (&a)[16],
-                                                 u32x4 (&b)[16]) {
-  auto compress_slot = [&](const u32x4 (&src)[16]) {
-    uint32_t mk[64];
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      mk[4 * g + 0] = src[g].x;
-      mk[4 * g + 1] = src[g].y;
-      mk[4 * g + 2] = src[g].z;
-      mk[4 * g + 3] = src[g].w;
-    }
-    md5_compress_mk(st, mk);
-  };
-#pragma unroll
-  for (int h = 0; h < kHalf; ++h) {
-    const bool cur_b = ((kPar + h) & 1) != 0;
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
-    // the next block's operands: this phase's, or the next phase's first
-    const uint32_t slot = h + 1 < kHalf ? s0 + h + 1 : s_next;
-    if (cur_b) pc_read_slot(a, ring, slot, lane); else pc_read_slot(b, ring, slot, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    if (kAllLive || blk0 + (uint32_t)h < nblk) {
-      if (cur_b) compress_slot(b); else compress_slot(a);
-    }
-  }
-}
 
 }  // namespace qsmd5
 
@@ -430,16 +387,14 @@ constexpr uint32_t kSkewMinBlocks = 1u << 19;
 // launch by the host, qsmd5_runtime.cpp load_nt_for).
 // kTrace (ubench only): the chain wave's lane 0 stamps s_memtime and
 // s_memrealtime every 4096 phases into trace[workgroup][2 * (p / 4096) + {0,1}].
-template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false,
-          int kRing = 2>
+template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
                                         uint32_t* __restrict__ digests, uint64_t col_off,
                                         uint64_t col_w, uint32_t* __restrict__ states,
                                         uint32_t skew, uint64_t* __restrict__ trace = nullptr,
                                         uint32_t lanes = 64) {
-  static_assert(kRing == 2 || (kRing >= 3 && !kTrace), "lead ring: no trace variant");
-  __shared__ u32x4 ring[kRing * kHalf][16][64];
+  __shared__ u32x4 ring[2 * kHalf][16][64];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wave = threadIdx.x >> 6;
   // `lanes` chains per workgroup (64, or fewer to spread long chains over more
@@ -477,52 +432,6 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     // ---------------- producer ----------------
     const uint32_t* base = reinterpret_cast<const uint32_t*>(pa & ~uintptr_t(3));
     const uint32_t last = nblk ? nblk - 1 : 0;
-    if constexpr (kRing >= 3) {
-      // lead ring: phases 0 and 1 before the first barrier, then phase p + 2
-      // during phase p, into half (p + 2) % kRing (read by the chain in
-      // phase p - 1, so free after the barrier that ended it).  Phase q's
-      // loads go into register set q % kDepth, issued kDepth writes earlier.
-      PcBlockRegs r[kDepth][kHalf];
-      auto load_q = [&](PcBlockRegs (&rs)[kHalf], uint32_t q) {
-        if (nblk && q < phases) {
-#pragma unroll
-          for (int h = 0; h < kHalf; ++h) {
-            const uint32_t j = q * kHalf + h;
-            pc_load_block<kNT>(rs[h], base, off, j < delta ? 0u : min(j - delta, last));
-          }
-        }
-      };
-      auto write_q = [&](const PcBlockRegs (&rs)[kHalf], uint32_t q) {
-        if (nblk) {
-#pragma unroll
-          for (int h = 0; h < kHalf; ++h) pc_write_mk(ring[(q % kRing) * kHalf + h], lane, rs[h], off);
-        }
-      };
-#pragma unroll
-      for (int q = 0; q < kDepth; ++q) load_q(r[q], (uint32_t)q);
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        if ((uint32_t)q < phases) {
-          write_q(r[q % kDepth], (uint32_t)q);
-          load_q(r[q % kDepth], (uint32_t)(q + kDepth));
-        }
-      }
-      lds_barrier();
-      for (uint32_t p0 = 0; p0 < phases; p0 += kDepth) {
-#pragma unroll
-        for (int u = 0; u < kDepth; ++u) {
-          const uint32_t p = p0 + (uint32_t)u;
-          if (p < phases) {
-            if (p + 2 < phases) {
-              write_q(r[(u + 2) % kDepth], p + 2);
-              load_q(r[(u + 2) % kDepth], p + 2 + kDepth);
-            }
-            lds_barrier();
-          }
-        }
-      }
-      return;
-    }
     // kDepth register sets of one phase each: the loads of phase q go into set
     // q % kDepth and are written to the ring kDepth phases after they were
     // issued, so a load has kDepth phases (~2 us each) to land.
@@ -582,26 +491,7 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     st[3] = s4.w;
   }
   lds_barrier();
-  if constexpr (kRing >= 3) {
-    u32x4 a[16], b[16];
-    pc_read_slot(a, ring, 0, lane);  // phase 0, block 0 (harmless if phases == 0)
-    // two phases per iteration so each block's register set is static
-    // (kHalf may be odd)
-    auto one = [&](uint32_t p, auto par) {
-      constexpr int kP = decltype(par)::value;
-      const uint32_t s0 = (p % kRing) * kHalf, sn = ((p + 1) % kRing) * kHalf;
-      if (p >= live_lo && p < live_hi)
-        chain_phase_lead<true, kHalf, kP>(st, ring, s0, sn, lane, p * kHalf - delta, nblk, a, b);
-      else
-        chain_phase_lead<false, kHalf, kP>(st, ring, s0, sn, lane, p * kHalf - delta, nblk, a, b);
-      lds_barrier();
-    };
-    for (uint32_t p = 0; p < phases; p += 2) {
-      one(p, std::integral_constant<int, 0>{});
-      if (p + 1 < phases) one(p + 1, std::integral_constant<int, kHalf & 1>{});
-    }
-  }
-  for (uint32_t p = 0; kRing == 2 && p < phases; ++p) {
+  for (uint32_t p = 0; p < phases; ++p) {
     if constexpr (kTrace) {
       if (lane == 0 && (p & 4095u) == 0u) {
         uint64_t* tr = trace + (uint64_t)blockIdx.x * 1024u + 2u * (p >> 12);

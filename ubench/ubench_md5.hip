@@ -151,14 +151,6 @@ __global__ __launch_bounds__(128) void k_chain_cost(uint64_t* out, uint32_t* sin
 
 // Latency kernel with 5-block phases: a 160 KiB ring (all of a gfx950 CU's
 // LDS), one barrier per 5 blocks instead of per 4.
-// lead ring: kRing halves of kH blocks, the producer two phases ahead
-template <int kH, int kR, int kD = 1>
-__global__ __launch_bounds__(128) void k_pc_lead(const ChunkDesc* __restrict__ c,
-                                                 const uint32_t* __restrict__ o, uint32_t n,
-                                                 uint32_t* __restrict__ d, uint32_t skew) {
-  pc_body<false, kD, kH, false, false, kR>(c, o, n, d, 0, ~0ull, nullptr, skew);
-}
-
 __global__ __launch_bounds__(128) void k_pc_half5(const ChunkDesc* __restrict__ c,
                                                   const uint32_t* __restrict__ o, uint32_t n,
                                                   uint32_t* __restrict__ d, uint32_t skew) {
@@ -375,21 +367,6 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 7)
       hipLaunchKernelGGL(k_pc_half5, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, 0u);
-    else if (which == 11)
-      hipLaunchKernelGGL((k_pc_lead<3, 3>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
-                         (uint32_t)B, d_dig, g_skew);
-    else if (which == 12)
-      hipLaunchKernelGGL((k_pc_lead<2, 3>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
-                         (uint32_t)B, d_dig, g_skew);
-    else if (which == 13)
-      hipLaunchKernelGGL((k_pc_lead<2, 4>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
-                         (uint32_t)B, d_dig, g_skew);
-    else if (which == 14)
-      hipLaunchKernelGGL((k_pc_lead<3, 3, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
-                         (uint32_t)B, d_dig, g_skew);
-    else if (which == 15)
-      hipLaunchKernelGGL((k_pc_lead<2, 4, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
-                         (uint32_t)B, d_dig, g_skew);
 
     else
       hipLaunchKernelGGL(k_pc_depth<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
@@ -418,7 +395,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 7 ? "pc-h5" : which == 11 ? "lead-3x3" : which == 12 ? "lead-2x3" : which == 13 ? "lead-2x4" : which == 14 ? "lead-3x3-d2" : which == 15 ? "lead-2x4-d2" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -498,21 +475,6 @@ static int run_edges(int which) {
   else if (which == 7)
     hipLaunchKernelGGL(k_pc_half5, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr, (uint32_t)n,
                        dg, 0u);
-  else if (which == 11)
-    hipLaunchKernelGGL((k_pc_lead<3, 3>), dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
-                       (uint32_t)n, dg, g_skew);
-  else if (which == 12)
-    hipLaunchKernelGGL((k_pc_lead<2, 3>), dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
-                       (uint32_t)n, dg, g_skew);
-  else if (which == 13)
-    hipLaunchKernelGGL((k_pc_lead<2, 4>), dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
-                       (uint32_t)n, dg, g_skew);
-  else if (which == 14)
-    hipLaunchKernelGGL((k_pc_lead<3, 3, 2>), dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
-                       (uint32_t)n, dg, g_skew);
-  else if (which == 15)
-    hipLaunchKernelGGL((k_pc_lead<2, 4, 2>), dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
-                       (uint32_t)n, dg, g_skew);
   else
     hipLaunchKernelGGL(k_pc_depth<3>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew);
@@ -1062,17 +1024,6 @@ int main(int argc, char** argv) {
       run_md5(512, 10ull << 20, 5, rep == 0, 1);
       run_md5(512, 10ull << 20, 5, rep == 0, 7);
     }
-    return bad ? 1 : 0;
-  }
-  if (!strcmp(mode, "lead")) {
-    // A/B: shipped ring (2 halves x 4 blocks) vs lead rings (the producer two
-    // phases ahead, next phase's first operands read during the last block),
-    // producer prefetch depth 1 or 2
-    int bad = run_edges(11) + run_edges(14) + run_edges(15);
-    for (int rep = 0; rep < 2; ++rep)
-      for (int w : {1, 3, 11, 14, 15}) run_md5(512, 10ull << 20, 7, rep == 0, w);
-    for (int w : {1, 14}) run_md5(512, 56ull << 20, 3, true, w);
-    for (int w : {1, 14, 15}) run_md5(8192, 1ull << 20, 5, true, w);
     return bad ? 1 : 0;
   }
   if (!strcmp(mode, "chaincost")) {
