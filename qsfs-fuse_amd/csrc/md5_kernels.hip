@@ -386,7 +386,11 @@ constexpr uint32_t kSkewMinBlocks = 1u << 19;
 // kNT: the producer's loads carry the non-temporal cache policy (chosen per
 // launch by the host, qsmd5_runtime.cpp load_nt_for).
 // kTrace (ubench only): the chain wave's lane 0 stamps s_memtime and
-// s_memrealtime every 4096 phases into trace[workgroup][2 * (p / 4096) + {0,1}].
+// s_memrealtime every 4096 phases into trace[workgroup][2 * (p / 4096) + {0,1}],
+// and at the end the cycles each wave spent: trace[workgroup][1019] producer
+// total, [1020] chain waiting at the phase barriers, [1021] chain total,
+// [1022] producer waiting at the barriers, [1023] producer writing the ring
+// (including its wait for the loads).
 template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
@@ -452,6 +456,8 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
           pc_write_mk(ring[(p & 1u) * kHalf + h], lane, rs[h], off);
       }
     };
+    uint64_t t_start = 0, t_wait = 0, t_write = 0;
+    if constexpr (kTrace) t_start = __builtin_amdgcn_s_memtime();
     if (phases > 0) {
 #pragma unroll
       for (int k = 0; k < kDepth; ++k) load_phase(r[k], (uint32_t)k);
@@ -467,11 +473,25 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
         const uint32_t p = p0 + (uint32_t)u;
         if (p < phases) {
           if (p + 1 < phases) {
+            uint64_t tw = 0;
+            if constexpr (kTrace) tw = __builtin_amdgcn_s_memtime();
             write_phase(r[(u + 1) % kDepth], p + 1);
+            if constexpr (kTrace) t_write += __builtin_amdgcn_s_memtime() - tw;
             load_phase(r[(u + 1) % kDepth], p + 1 + kDepth);
           }
+          uint64_t tb = 0;
+          if constexpr (kTrace) tb = __builtin_amdgcn_s_memtime();
           lds_barrier();
+          if constexpr (kTrace) t_wait += __builtin_amdgcn_s_memtime() - tb;
         }
+      }
+    }
+    if constexpr (kTrace) {
+      if (lane == 0) {
+        uint64_t* tr = trace + (uint64_t)blockIdx.x * 1024u;
+        tr[1019] = __builtin_amdgcn_s_memtime() - t_start;
+        tr[1022] = t_wait;
+        tr[1023] = t_write;
       }
     }
     return;
@@ -490,6 +510,8 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     st[2] = s4.z;
     st[3] = s4.w;
   }
+  uint64_t c_start = 0, c_wait = 0;
+  if constexpr (kTrace) c_start = __builtin_amdgcn_s_memtime();
   lds_barrier();
   for (uint32_t p = 0; p < phases; ++p) {
     if constexpr (kTrace) {
@@ -504,7 +526,17 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
       chain_phase<true, kHalf>(st, ring, s0, lane, p * kHalf - delta, nblk);
     else
       chain_phase<false, kHalf>(st, ring, s0, lane, p * kHalf - delta, nblk);
+    uint64_t tb = 0;
+    if constexpr (kTrace) tb = __builtin_amdgcn_s_memtime();
     lds_barrier();
+    if constexpr (kTrace) c_wait += __builtin_amdgcn_s_memtime() - tb;
+  }
+  if constexpr (kTrace) {
+    if (lane == 0) {
+      uint64_t* tr = trace + (uint64_t)blockIdx.x * 1024u;
+      tr[1020] = c_wait;
+      tr[1021] = __builtin_amdgcn_s_memtime() - c_start;
+    }
   }
   if (!live) return;
   if (kColumn && !final) {

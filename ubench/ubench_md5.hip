@@ -997,7 +997,19 @@ int main(int argc, char** argv) {
     printf("ptrace B=%d L=%llu MiB pad=%llu skew=%u lanes=%u: %.2f ms, %.1f cycles/block overall at 2.4 GHz\n",
            B, (unsigned long long)(L >> 20), (unsigned long long)pad, g_skew, lanes, ms,
            ms * 1e-3 * 2.4e9 / (double)nblk);
-    const int pts = (int)std::min<uint64_t>(512, (nblk / 4 + 4095) / 4096);
+    {
+      // where the waves' cycles go, per phase (4 blocks), averaged over workgroups
+      double cw = 0, ct = 0, pw = 0, pwr = 0, pt = 0;
+      for (int g = 0; g < groups; ++g) {
+        const uint64_t* t = &tr[(uint64_t)g * 1024];
+        pt += t[1019]; cw += t[1020]; ct += t[1021]; pw += t[1022]; pwr += t[1023];
+      }
+      const double ph = (double)groups * (double)(nblk / 4);
+      printf("  per phase: chain %.0f cycles (%.0f waiting at the barrier); producer %.0f "
+             "(%.0f writing the ring incl. load waits, %.0f at the barrier)\n",
+             ct / ph, cw / ph, pt / ph, pwr / ph, pw / ph);
+    }
+    const int pts = (int)std::min<uint64_t>(510, (nblk / 4 + 4095) / 4096);
     for (int g = 0; g < groups; g += std::max(1, groups / 4)) {
       printf("  wg %d: MiB-index:cycles/block@GHz", g);
       for (int k = 1; k < pts; ++k) {
