@@ -248,7 +248,7 @@ def main():
     desc = desc.to(dev)
     dig = torch.zeros((B, 16), dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
-    kernel = {0: "one-wave (qsmd5_batch_kernel)", 1: "producer/consumer (qsmd5_batch_pc_kernel)",
+    kernel = {0: "one-wave (qsmd5_batch_kernel)", 1: "producer/consumer (qsmd5_batch_pc64_kernel)",
               2: "coalesced (qsmd5_batch_coal_kernel)",
               3: "producer/consumer, 64 KiB ring (qsmd5_batch_pc2_kernel)"}[qsmd5.kernel_choice(B)]
 

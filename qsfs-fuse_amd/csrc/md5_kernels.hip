@@ -6,7 +6,9 @@
 //   qsmd5_batch_pc_kernel    latency kernel, <= 256 x 64 chunks (every
 //                            BASELINE config): producer wave streams blocks and
 //                            precomputes x[g]+K into LDS, chain wave runs only
-//                            the serial 4-VALU steps.
+//                            the serial 4-VALU steps.  qsmd5_batch_pc64/32_kernel
+//                            are the same with 64 / 32 chains per workgroup
+//                            fixed at compile time (what the runtime launches).
 //   qsmd5_batch_pc2_kernel   the same with a 64 KiB ring (two workgroups per
 //                            CU): <= 2 x 256 x 64 chunks.
 //   qsmd5_batch_coal_kernel  throughput kernel, more chunks, 16-B aligned:
@@ -391,7 +393,8 @@ constexpr uint32_t kSkewMinBlocks = 1u << 19;
 // total, [1020] chain waiting at the phase barriers, [1021] chain total,
 // [1022] producer waiting at the barriers, [1023] producer writing the ring
 // (including its wait for the loads).
-template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false>
+template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false,
+          int kPace = 0, int kGap = 0>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
                                         uint32_t* __restrict__ digests, uint64_t col_off,
@@ -452,8 +455,12 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     auto write_phase = [&](const PcBlockRegs (&rs)[kHalf], uint32_t p) {
       if (nblk) {
 #pragma unroll
-        for (int h = 0; h < kHalf; ++h)
+        for (int h = 0; h < kHalf; ++h) {
+          if constexpr (kGap > 0) {
+            if (h) __builtin_amdgcn_s_sleep(kGap);
+          }
           pc_write_mk(ring[(p & 1u) * kHalf + h], lane, rs[h], off);
+        }
       }
     };
     uint64_t t_start = 0, t_wait = 0, t_write = 0;
@@ -475,6 +482,7 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
           if (p + 1 < phases) {
             uint64_t tw = 0;
             if constexpr (kTrace) tw = __builtin_amdgcn_s_memtime();
+            if constexpr (kPace > 0) __builtin_amdgcn_s_sleep(kPace);
             write_phase(r[(u + 1) % kDepth], p + 1);
             if constexpr (kTrace) t_write += __builtin_amdgcn_s_memtime() - tw;
             load_phase(r[(u + 1) % kDepth], p + 1 + kDepth);
@@ -549,11 +557,36 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
   *reinterpret_cast<u32x4*>(digests + 4u * (uint64_t)idx) = o;
 }
 
+// Whole-chunk batches: producer loads two phases ahead (kDepth 2) and, after
+// each phase barrier, a ~512-cycle pause before it writes the next phase, so
+// its 64 ring writes do not queue ahead of the chain's first operand reads of
+// the phase: 1200 against 1210-1219 cycles per block at 512 x 10 MiB
+// (profiles/r02_pace_ab.log).  Longer pauses make the producer late.
+constexpr int kPcDepth = 2;
+constexpr int kPcPace = 8;  // s_sleep units of 64 cycles
+
 extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
     uint32_t* __restrict__ digests, uint32_t skew, uint32_t lanes) {
-  pc_body<false>(chunks, order, n, digests, 0, ~0ull, nullptr, skew, nullptr, lanes);
+  pc_body<false, kPcDepth, kPcHalf, false, false, kPcPace>(chunks, order, n, digests, 0, ~0ull,
+                                                           nullptr, skew, nullptr, lanes);
 }
+
+// The same kernel with the lanes per workgroup fixed at compile time (the
+// runtime's two choices, 64 and 32): the lane bounds fold away, worth ~1% of
+// the chain's cycles at 512 x 10 MiB (profiles/r02_pace_ab.log).
+#define QSMD5_PC_FIXED(NAME, LANES, NT)                                                        \
+  extern "C" __global__ __launch_bounds__(128) void NAME(                                     \
+      const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,   \
+      uint32_t* __restrict__ digests, uint32_t skew) {                                        \
+    pc_body<false, kPcDepth, kPcHalf, NT, false, kPcPace>(chunks, order, n, digests, 0, ~0ull, \
+                                                          nullptr, skew, nullptr, LANES);      \
+  }
+QSMD5_PC_FIXED(qsmd5_batch_pc64_kernel, 64u, false)
+QSMD5_PC_FIXED(qsmd5_batch_pc64_nt_kernel, 64u, true)
+QSMD5_PC_FIXED(qsmd5_batch_pc32_kernel, 32u, false)
+QSMD5_PC_FIXED(qsmd5_batch_pc32_nt_kernel, 32u, true)
+#undef QSMD5_PC_FIXED
 
 // 2-block phases: a 64 KiB ring, so two workgroups (four waves) share a CU and
 // one launch keeps 2 x 256 x 64 chunks resident (kKernelLatency2).
@@ -567,7 +600,8 @@ extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc2_kernel(
 extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc_nt_kernel(
     const ChunkDesc* __restrict__ chunks, const uint32_t* __restrict__ order, uint32_t n,
     uint32_t* __restrict__ digests, uint32_t skew, uint32_t lanes) {
-  pc_body<false, 1, kPcHalf, true>(chunks, order, n, digests, 0, ~0ull, nullptr, skew, nullptr, lanes);
+  pc_body<false, kPcDepth, kPcHalf, true, false, kPcPace>(chunks, order, n, digests, 0, ~0ull,
+                                                          nullptr, skew, nullptr, lanes);
 }
 
 extern "C" __global__ __launch_bounds__(128) void qsmd5_batch_pc2_nt_kernel(
@@ -849,9 +883,17 @@ hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, u
   if (lanes < 1 || lanes > 64) return hipErrorInvalidValue;
   const uint32_t pc_groups = (n + lanes - 1) / lanes;
   if (kind == kKernelLatency) {
-    hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc_nt_kernel : qsmd5_batch_pc_kernel, dim3(pc_groups),
-                       dim3(128), 0, s, static_cast<const ChunkDesc*>(chunks), order, n, digests,
-                       skew_blocks / kPcHalf * kPcHalf, lanes);
+    const ChunkDesc* c = static_cast<const ChunkDesc*>(chunks);
+    const uint32_t skew = skew_blocks / kPcHalf * kPcHalf;
+    if (lanes == 64)
+      hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc64_nt_kernel : qsmd5_batch_pc64_kernel,
+                         dim3(pc_groups), dim3(128), 0, s, c, order, n, digests, skew);
+    else if (lanes == 32)
+      hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc32_nt_kernel : qsmd5_batch_pc32_kernel,
+                         dim3(pc_groups), dim3(128), 0, s, c, order, n, digests, skew);
+    else
+      hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc_nt_kernel : qsmd5_batch_pc_kernel, dim3(pc_groups),
+                         dim3(128), 0, s, c, order, n, digests, skew, lanes);
   } else if (kind == kKernelLatency2) {
     hipLaunchKernelGGL(load_nt ? qsmd5_batch_pc2_nt_kernel : qsmd5_batch_pc2_kernel, dim3(pc_groups),
                        dim3(128), 0, s, static_cast<const ChunkDesc*>(chunks), order, n, digests,

@@ -45,11 +45,11 @@ def main(rnd):
     factor = cal_bytes / (statistics.median(cal_kib) * 1024.0)
 
     bench_pmc = os.path.join(RAW, "pmc_bench", "pmc_counter_collection.csv")
-    pc_kib = fetch_kib(bench_pmc, "qsmd5_batch_pc_kernel")
+    pc_kib = fetch_kib(bench_pmc, "qsmd5_batch_pc64_kernel")
     alg = 512 * 10485760
     hbm = statistics.median(pc_kib) * 1024.0 * factor
     traffic = {
-        "workload": "batch512x10MiB", "kernel": "qsmd5_batch_pc_kernel",
+        "workload": "batch512x10MiB", "kernel": "qsmd5_batch_pc64_kernel",
         "source": "rocprofv3 --pmc FETCH_SIZE -- python3 bench.py --no-cpu-baseline --steps 2 "
                   "--warmup 1 (own pass, no trace domains); raw: profiles/%s_pmc_fetch_size_bench.csv" % rnd,
         "fetch_size_kib_raw_per_launch": statistics.median(pc_kib), "launches": len(pc_kib),

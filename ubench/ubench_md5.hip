@@ -52,7 +52,8 @@ __global__ __launch_bounds__(128) void k_pc_trace(const ChunkDesc* __restrict__ 
                                                   const uint32_t* __restrict__ o, uint32_t n,
                                                   uint32_t* __restrict__ d, uint32_t skew,
                                                   uint64_t* __restrict__ tr, uint32_t lanes) {
-  pc_body<false, 1, kPcHalf, false, true>(c, o, n, d, 0, ~0ull, nullptr, skew, tr, lanes);
+  pc_body<false, kPcDepth, kPcHalf, false, true, kPcPace>(c, o, n, d, 0, ~0ull, nullptr, skew, tr,
+                                                          lanes);
 }
 
 // chain_phase with the 16 LDS reads of block h+1 spread through block h's 256
@@ -151,6 +152,16 @@ __global__ __launch_bounds__(128) void k_chain_cost(uint64_t* out, uint32_t* sin
 
 // Latency kernel with 5-block phases: a 160 KiB ring (all of a gfx950 CU's
 // LDS), one barrier per 5 blocks instead of per 4.
+// producer sleeps kP x ~64 cycles after each phase barrier before writing the
+// ring, so the chain's first operand reads of the phase are not queued behind
+// the producer's 64 ds_write_b128
+template <int kP, int kG = 0, int kD = 1>
+__global__ __launch_bounds__(128) void k_pc_pace(const ChunkDesc* __restrict__ c,
+                                                 const uint32_t* __restrict__ o, uint32_t n,
+                                                 uint32_t* __restrict__ d, uint32_t skew) {
+  pc_body<false, kD, kPcHalf, false, false, kP, kG>(c, o, n, d, 0, ~0ull, nullptr, skew);
+}
+
 __global__ __launch_bounds__(128) void k_pc_half5(const ChunkDesc* __restrict__ c,
                                                   const uint32_t* __restrict__ o, uint32_t n,
                                                   uint32_t* __restrict__ d, uint32_t skew) {
@@ -349,7 +360,10 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     if (which == 0)
       hipLaunchKernelGGL(qsmd5_batch_kernel, dim3(grid), dim3(64), 0, 0, d_desc, nullptr,
                          (uint32_t)B, d_dig);
-    else if (which == 1)
+    else if (which == 1)  // what the runtime launches at 64 chains per workgroup
+      hipLaunchKernelGGL(qsmd5_batch_pc64_kernel, dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 19)  // the same kernel with the lanes per workgroup a runtime argument
       hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
                          (uint32_t)B, d_dig, g_skew, 64u);
     else if (which == 2)
@@ -367,7 +381,27 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 7)
       hipLaunchKernelGGL(k_pc_half5, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, 0u);
-
+    else if (which == 20)
+      hipLaunchKernelGGL((k_pc_pace<0,0,1>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 21)
+      hipLaunchKernelGGL((k_pc_pace<8,0,1>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 22)
+      hipLaunchKernelGGL((k_pc_pace<10,0,1>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 23)
+      hipLaunchKernelGGL((k_pc_pace<8,0,2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 24)
+      hipLaunchKernelGGL((k_pc_pace<16,0,2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 25)
+      hipLaunchKernelGGL((k_pc_pace<24,0,2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 26)
+      hipLaunchKernelGGL((k_pc_pace<32,0,2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
     else
       hipLaunchKernelGGL(k_pc_depth<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
@@ -395,7 +429,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 19 ? "pc (runtime lanes)" : which == 20 ? "pc-r1 (depth 1, no pause)" : which == 21 ? "pace8" : which == 22 ? "pace10" : which == 23 ? "d2-pace8" : which == 24 ? "d2-pace16" : which == 25 ? "d2-pace24" : which == 26 ? "d2-pace32" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -458,6 +492,9 @@ static int run_edges(int which) {
     hipLaunchKernelGGL(qsmd5_batch_kernel, dim3((n + 63) / 64), dim3(64), 0, 0, dd, nullptr,
                        (uint32_t)n, dg);
   else if (which == 1)
+    hipLaunchKernelGGL(qsmd5_batch_pc64_kernel, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
+                       (uint32_t)n, dg, g_skew);
+  else if (which == 19)
     hipLaunchKernelGGL(qsmd5_batch_pc_kernel, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew, 64u);
   else if (which == 2)
@@ -475,6 +512,12 @@ static int run_edges(int which) {
   else if (which == 7)
     hipLaunchKernelGGL(k_pc_half5, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr, (uint32_t)n,
                        dg, 0u);
+  else if (which == 21)
+    hipLaunchKernelGGL((k_pc_pace<8, 0, 1>), dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
+                       (uint32_t)n, dg, g_skew);
+  else if (which == 24)
+    hipLaunchKernelGGL((k_pc_pace<16, 0, 2>), dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
+                       (uint32_t)n, dg, g_skew);
   else
     hipLaunchKernelGGL(k_pc_depth<3>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew);
@@ -1036,6 +1079,15 @@ int main(int argc, char** argv) {
       run_md5(512, 10ull << 20, 5, rep == 0, 1);
       run_md5(512, 10ull << 20, 5, rep == 0, 7);
     }
+    return bad ? 1 : 0;
+  }
+  if (!strcmp(mode, "pace")) {
+    // A/B: the shipped producer (pc: depth 2, ~512-cycle pause before it writes
+    // the ring) vs round 1's (depth 1, no pause) and other pauses
+    int bad = run_edges(1) + run_edges(19);
+    for (int rep = 0; rep < 3; ++rep)
+      for (int w : {1, 19, 20, 23}) run_md5(512, 10ull << 20, 7, rep == 0, w);
+    for (int w : {1, 19, 20}) run_md5(8192, 1ull << 20, 5, true, w);
     return bad ? 1 : 0;
   }
   if (!strcmp(mode, "chaincost")) {
