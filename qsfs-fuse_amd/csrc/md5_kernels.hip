@@ -194,6 +194,10 @@ __device__ __forceinline__ void lds_barrier() {
 // serial part: 4 VALU per step plus one ds_read_b128 per 4 steps.  The two waves
 // sit on different SIMDs, so the chain wave's issue slots are not shared.
 constexpr int kPcHalf = 4;  // blocks per ring half (one phase): 8 x 16 KiB = 128 KiB of LDS
+// Steps of each phase's first block that run on its first kPcLead / 4 operand
+// reads (chain_phase kLead): 1188-1192 against 1199-1202 cycles per block at
+// 512 x 10 MiB, 1195 against 1208 at 8192 x 1 MiB (profiles/r02_lead_ab.log).
+constexpr int kPcLead = 8;
 // s_waitcnt immediate (gfx9 encoding) for lgkmcnt(0) alone: vmcnt 63, expcnt 7.
 constexpr int kLgkmcnt0 = 0xC07F;
 
@@ -236,7 +240,12 @@ __device__ __forceinline__ void pc_write_mk(u32x4 (*slot)[64], uint32_t lane, co
 // One phase of the chain wave: kPcHalf blocks from ring slots s0.., the
 // operands of block h+1 read from LDS while block h compresses.  kAllLive
 // drops the per-block lane predicate (every lane has blocks blk0..blk0+H-1).
-template <bool kAllLive, int kHalf = kPcHalf>
+//
+// kLead > 0: the first block of the phase, whose 16 reads go out right after
+// the phase barrier, waits only for its first kLead/4 reads (LDS returns in
+// order), runs steps [0, kLead), then waits for the rest and sends block 1's
+// reads.  The full-block wait exposes all 16 reads' latency once per phase.
+template <bool kAllLive, int kHalf = kPcHalf, int kLead = 0, int kLead2 = 0>
 __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*ring)[16][64],
                                             uint32_t s0, uint32_t lane, uint32_t blk0,
                                             uint32_t nblk) {
@@ -245,8 +254,7 @@ __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*rin
 #pragma unroll
     for (int g = 0; g < 16; ++g) dst[g] = ring[slot][g][lane];
   };
-  auto compress_slot = [&](const u32x4 (&src)[16]) {
-    uint32_t mk[64];
+  auto unpack_slot = [&](uint32_t (&mk)[64], const u32x4 (&src)[16]) {
 #pragma unroll
     for (int g = 0; g < 16; ++g) {
       mk[4 * g + 0] = src[g].x;
@@ -254,11 +262,46 @@ __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*rin
       mk[4 * g + 2] = src[g].z;
       mk[4 * g + 3] = src[g].w;
     }
+  };
+  auto compress_slot = [&](const u32x4 (&src)[16]) {
+    uint32_t mk[64];
+    unpack_slot(mk, src);
     md5_compress_mk(st, mk);
   };
   read_slot(a, s0);
+  if constexpr (kLead > 0) {
+    static_assert(kLead % 4 == 0 && kLead < 64, "kLead: whole ds_read_b128 groups");
+    // block 0 with a graded wait; blocks 1.. below as usual
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kLgkmcnt0 & ~(0xF << 8) | ((16 - kLead / 4) << 8));
+    __builtin_amdgcn_sched_barrier(0);
+    const bool run0 = kAllLive || blk0 < nblk;
+    uint32_t mk[64];
+    unpack_slot(mk, a);
+    uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+    if (run0) md5_steps_mk<0, kLead>(v, mk);
+    constexpr int kRest = kLead2 > kLead ? kLead2 : kLead;
+    if constexpr (kLead2 > kLead) {
+      static_assert(kLead2 % 4 == 0 && kLead2 < 64, "kLead2: whole ds_read_b128 groups");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_waitcnt(kLgkmcnt0 & ~(0xF << 8) | ((16 - kLead2 / 4) << 8));
+      __builtin_amdgcn_sched_barrier(0);
+      if (run0) md5_steps_mk<kLead, kLead2>(v, mk);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
+    if (1 < kHalf) read_slot(b, s0 + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (run0) {
+      md5_steps_mk<kRest, 64>(v, mk);
+      st[0] += v[0];
+      st[1] += v[1];
+      st[2] += v[2];
+      st[3] += v[3];
+    }
+  }
 #pragma unroll
-  for (int h = 0; h < kHalf; ++h) {
+  for (int h = (kLead > 0 ? 1 : 0); h < kHalf; ++h) {
     // One wait per block: the operands of block h (read a whole block ago)
     // are complete, then the 16 reads of block h+1 go out and the 256 VALU of
     // block h need no wait at all.  Left to itself the compiler hoists two
@@ -394,7 +437,7 @@ constexpr uint32_t kSkewMinBlocks = 1u << 19;
 // [1022] producer waiting at the barriers, [1023] producer writing the ring
 // (including its wait for the loads).
 template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false,
-          int kPace = 0, int kGap = 0>
+          int kPace = 0, int kGap = 0, int kLead = kPcLead, int kLead2 = 0>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
                                         uint32_t* __restrict__ digests, uint64_t col_off,
@@ -531,9 +574,9 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     }
     const uint32_t s0 = (p & 1u) * kHalf;
     if (p >= live_lo && p < live_hi)
-      chain_phase<true, kHalf>(st, ring, s0, lane, p * kHalf - delta, nblk);
+      chain_phase<true, kHalf, kLead, kLead2>(st, ring, s0, lane, p * kHalf - delta, nblk);
     else
-      chain_phase<false, kHalf>(st, ring, s0, lane, p * kHalf - delta, nblk);
+      chain_phase<false, kHalf, kLead, kLead2>(st, ring, s0, lane, p * kHalf - delta, nblk);
     uint64_t tb = 0;
     if constexpr (kTrace) tb = __builtin_amdgcn_s_memtime();
     lds_barrier();

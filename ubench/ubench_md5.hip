@@ -117,7 +117,7 @@ __global__ __launch_bounds__(128) void k_chain_spread(uint64_t* out, uint32_t* s
 //            only meets the barriers (the producer's role without its loads)
 //   kMode 2: md5_compress_mk from registers (no LDS reads at all)
 // out[0] = s_memtime cycles of the chain wave over `phases` phases of 4 blocks.
-template <int kMode, uint32_t kLanes = 64>
+template <int kMode, uint32_t kLanes = 64, int kL = 0>
 __global__ __launch_bounds__(128) void k_chain_cost(uint64_t* out, uint32_t* sink, int phases) {
   __shared__ u32x4 ring[2 * kPcHalf][16][64];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(128) void k_chain_cost(uint64_t* out, uint32_t* sin
       for (int h = 0; h < kPcHalf; ++h) md5_compress_mk(st, mk);
       asm volatile("" : "+v"(st[0]), "+v"(st[1]));
     } else {
-      chain_phase<true>(st, ring, (uint32_t)(p & 1) * kPcHalf, lane, 0, 1u << 30);
+      chain_phase<true, kPcHalf, kL>(st, ring, (uint32_t)(p & 1) * kPcHalf, lane, 0, 1u << 30);
       if (kMode == 1) lds_barrier();
     }
   }
@@ -160,6 +160,16 @@ __global__ __launch_bounds__(128) void k_pc_pace(const ChunkDesc* __restrict__ c
                                                  const uint32_t* __restrict__ o, uint32_t n,
                                                  uint32_t* __restrict__ d, uint32_t skew) {
   pc_body<false, kD, kPcHalf, false, false, kP, kG>(c, o, n, d, 0, ~0ull, nullptr, skew);
+}
+
+// Graded wait at each phase's first block (chain_phase kLead): the shipped
+// producer (depth 2, pause 8) and 64 lanes fixed, as qsmd5_batch_pc64_kernel.
+template <int kL, int kL2 = 0>
+__global__ __launch_bounds__(128) void k_pc_lead(const ChunkDesc* __restrict__ c,
+                                                 const uint32_t* __restrict__ o, uint32_t n,
+                                                 uint32_t* __restrict__ d, uint32_t skew) {
+  pc_body<false, 2, kPcHalf, false, false, 8, 0, kL, kL2>(c, o, n, d, 0, ~0ull, nullptr, skew, nullptr,
+                                                      64u);
 }
 
 __global__ __launch_bounds__(128) void k_pc_half5(const ChunkDesc* __restrict__ c,
@@ -402,6 +412,21 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 26)
       hipLaunchKernelGGL((k_pc_pace<32,0,2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
+    else if (which == 30)
+      hipLaunchKernelGGL(k_pc_lead<8>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 31)
+      hipLaunchKernelGGL((k_pc_lead<8, 24>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 32)
+      hipLaunchKernelGGL((k_pc_lead<4, 16>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 34)
+      hipLaunchKernelGGL((k_pc_lead<0>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 33)
+      hipLaunchKernelGGL((k_pc_lead<8, 32>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
     else
       hipLaunchKernelGGL(k_pc_depth<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
@@ -429,7 +454,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 19 ? "pc (runtime lanes)" : which == 20 ? "pc-r1 (depth 1, no pause)" : which == 21 ? "pace8" : which == 22 ? "pace10" : which == 23 ? "d2-pace8" : which == 24 ? "d2-pace16" : which == 25 ? "d2-pace24" : which == 26 ? "d2-pace32" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 19 ? "pc (runtime lanes)" : which == 20 ? "pc-r1 (depth 1, no pause)" : which == 21 ? "pace8" : which == 22 ? "pace10" : which == 23 ? "d2-pace8" : which == 24 ? "d2-pace16" : which == 25 ? "d2-pace24" : which == 26 ? "d2-pace32" : which == 30 ? "lead8" : which == 31 ? "lead8+24" : which == 32 ? "lead4+16" : which == 33 ? "lead8+32" : which == 34 ? "lead0 (no graded wait)" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -518,7 +543,11 @@ static int run_edges(int which) {
   else if (which == 24)
     hipLaunchKernelGGL((k_pc_pace<16, 0, 2>), dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew);
-  else
+  else if (which >= 30 && which <= 33) {
+    auto k = which == 30 ? k_pc_lead<8> : which == 31 ? k_pc_lead<8, 24>
+           : which == 32 ? k_pc_lead<4, 16> : k_pc_lead<8, 32>;
+    hipLaunchKernelGGL(k, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr, (uint32_t)n, dg, g_skew);
+  } else
     hipLaunchKernelGGL(k_pc_depth<3>, dim3((n + 63) / 64), dim3(128), 0, 0, dd, nullptr,
                        (uint32_t)n, dg, g_skew);
   CK(hipDeviceSynchronize());
@@ -1090,6 +1119,20 @@ int main(int argc, char** argv) {
     for (int w : {1, 19, 20}) run_md5(8192, 1ull << 20, 5, true, w);
     return bad ? 1 : 0;
   }
+  if (!strcmp(mode, "lead")) {
+    // A/B: chain_phase's graded wait at each phase's first block (kLead steps
+    // on the first kLead/4 reads) against the shipped qsmd5_batch_pc64_kernel
+    // (the shipped kernel, which 1, runs lead 8 since this A/B; which 34 is
+    // the kernel before it)
+    int bad = 0;
+    for (int w : {30, 31, 32, 33}) bad += run_edges(w);
+    for (int rep = 0; rep < 3; ++rep)
+      for (int w : {1, 34}) run_md5(512, 10ull << 20, 7, rep == 0, w);
+    for (int rep = 0; rep < 4; ++rep)
+      for (int w : {1, 30, 31, 32, 33}) run_md5(512, 10ull << 20, 7, rep == 0, w);
+    for (int w : {1, 30, 31, 32, 33}) run_md5(8192, 1ull << 20, 5, true, w);
+    return bad ? 1 : 0;
+  }
   if (!strcmp(mode, "chaincost")) {
     // cycles per 64-B block of the chain wave, by what it does besides the steps
     uint64_t* d_out;
@@ -1113,6 +1156,11 @@ int main(int argc, char** argv) {
     one(k_chain_cost<0, 1>, "chain_phase, 1 active lane");
     one(k_chain_cost<2, 32>, "steps from registers, 32 active lanes");
     one(k_chain_spread<16>, "reads spread: 1 DS read per 16 VALU");
+    one(k_chain_cost<0, 64, 4>, "chain_phase, graded wait on block 0 (lead 4 steps)");
+    one(k_chain_cost<0, 64, 8>, "chain_phase, graded wait on block 0 (lead 8 steps)");
+    one(k_chain_cost<0, 64, 16>, "chain_phase, graded wait on block 0 (lead 16 steps)");
+    one(k_chain_cost<0, 64, 32>, "chain_phase, graded wait on block 0 (lead 32 steps)");
+    one(k_chain_cost<1, 64, 16>, "+ lds_barrier per 4 blocks, lead 16");
     CK(hipFree(d_out));
     CK(hipFree(d_sink));
     return 0;
