@@ -164,11 +164,11 @@ __global__ __launch_bounds__(128) void k_pc_pace(const ChunkDesc* __restrict__ c
 
 // Graded wait at each phase's first block (chain_phase kLead): the shipped
 // producer (depth 2, pause 8) and 64 lanes fixed, as qsmd5_batch_pc64_kernel.
-template <int kL, int kL2 = 0>
+template <int kL, int kL2 = 0, int kP = 8, int kD = 2>
 __global__ __launch_bounds__(128) void k_pc_lead(const ChunkDesc* __restrict__ c,
                                                  const uint32_t* __restrict__ o, uint32_t n,
                                                  uint32_t* __restrict__ d, uint32_t skew) {
-  pc_body<false, 2, kPcHalf, false, false, 8, 0, kL, kL2>(c, o, n, d, 0, ~0ull, nullptr, skew, nullptr,
+  pc_body<false, kD, kPcHalf, false, false, kP, 0, kL, kL2>(c, o, n, d, 0, ~0ull, nullptr, skew, nullptr,
                                                       64u);
 }
 
@@ -421,6 +421,21 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 32)
       hipLaunchKernelGGL((k_pc_lead<4, 16>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
+    else if (which == 35)
+      hipLaunchKernelGGL((k_pc_lead<8, 0, 4, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 36)
+      hipLaunchKernelGGL((k_pc_lead<8, 0, 12, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 37)
+      hipLaunchKernelGGL((k_pc_lead<8, 0, 8, 3>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 38)
+      hipLaunchKernelGGL((k_pc_lead<8, 0, 16, 3>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 39)
+      hipLaunchKernelGGL((k_pc_lead<8, 0, 0, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
     else if (which == 34)
       hipLaunchKernelGGL((k_pc_lead<0>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
@@ -454,7 +469,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 19 ? "pc (runtime lanes)" : which == 20 ? "pc-r1 (depth 1, no pause)" : which == 21 ? "pace8" : which == 22 ? "pace10" : which == 23 ? "d2-pace8" : which == 24 ? "d2-pace16" : which == 25 ? "d2-pace24" : which == 26 ? "d2-pace32" : which == 30 ? "lead8" : which == 31 ? "lead8+24" : which == 32 ? "lead4+16" : which == 33 ? "lead8+32" : which == 34 ? "lead0 (no graded wait)" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 19 ? "pc (runtime lanes)" : which == 20 ? "pc-r1 (depth 1, no pause)" : which == 21 ? "pace8" : which == 22 ? "pace10" : which == 23 ? "d2-pace8" : which == 24 ? "d2-pace16" : which == 25 ? "d2-pace24" : which == 26 ? "d2-pace32" : which == 30 ? "lead8" : which == 31 ? "lead8+24" : which == 32 ? "lead4+16" : which == 33 ? "lead8+32" : which == 34 ? "lead0 (no graded wait)" : which == 35 ? "lead8 pace4" : which == 36 ? "lead8 pace12" : which == 37 ? "lead8 pace8 depth3" : which == 38 ? "lead8 pace16 depth3" : which == 39 ? "lead8 no pause" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -1132,6 +1147,13 @@ int main(int argc, char** argv) {
       for (int w : {1, 30, 31, 32, 33}) run_md5(512, 10ull << 20, 7, rep == 0, w);
     for (int w : {1, 30, 31, 32, 33}) run_md5(8192, 1ull << 20, 5, true, w);
     return bad ? 1 : 0;
+  }
+  if (!strcmp(mode, "lead_pace")) {
+    // with the graded wait shipped: producer pause and depth again
+    for (int rep = 0; rep < 3; ++rep)
+      for (int w : {1, 35, 36, 37, 38, 39}) run_md5(512, 10ull << 20, 7, rep == 0, w);
+    for (int w : {1, 37, 38}) run_md5(8192, 1ull << 20, 5, true, w);
+    return 0;
   }
   if (!strcmp(mode, "chaincost")) {
     // cycles per 64-B block of the chain wave, by what it does besides the steps
