@@ -172,6 +172,15 @@ __global__ __launch_bounds__(128) void k_pc_lead(const ChunkDesc* __restrict__ c
                                                       64u);
 }
 
+// 64 KiB-ring latency kernel (2-block phases) with the whole-chunk producer
+// options of the 128 KiB kernel: pause kP after each barrier, depth kD
+template <int kP, int kD>
+__global__ __launch_bounds__(128) void k_pc2_pace(const ChunkDesc* __restrict__ c,
+                                                  const uint32_t* __restrict__ o, uint32_t n,
+                                                  uint32_t* __restrict__ d, uint32_t skew) {
+  pc_body<false, kD, 2, false, false, kP>(c, o, n, d, 0, ~0ull, nullptr, skew, nullptr, 64u);
+}
+
 __global__ __launch_bounds__(128) void k_pc_half5(const ChunkDesc* __restrict__ c,
                                                   const uint32_t* __restrict__ o, uint32_t n,
                                                   uint32_t* __restrict__ d, uint32_t skew) {
@@ -436,6 +445,21 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 39)
       hipLaunchKernelGGL((k_pc_lead<8, 0, 0, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
                          (uint32_t)B, d_dig, g_skew);
+    else if (which == 40)
+      hipLaunchKernelGGL((k_pc2_pace<0, 1>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 41)
+      hipLaunchKernelGGL((k_pc2_pace<0, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 42)
+      hipLaunchKernelGGL((k_pc2_pace<4, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 43)
+      hipLaunchKernelGGL((k_pc2_pace<8, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
+    else if (which == 44)
+      hipLaunchKernelGGL((k_pc2_pace<2, 2>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr,
+                         (uint32_t)B, d_dig, g_skew);
     else if (which == 34)
       hipLaunchKernelGGL((k_pc_lead<0>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
@@ -469,7 +493,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 19 ? "pc (runtime lanes)" : which == 20 ? "pc-r1 (depth 1, no pause)" : which == 21 ? "pace8" : which == 22 ? "pace10" : which == 23 ? "d2-pace8" : which == 24 ? "d2-pace16" : which == 25 ? "d2-pace24" : which == 26 ? "d2-pace32" : which == 30 ? "lead8" : which == 31 ? "lead8+24" : which == 32 ? "lead4+16" : which == 33 ? "lead8+32" : which == 34 ? "lead0 (no graded wait)" : which == 35 ? "lead8 pace4" : which == 36 ? "lead8 pace12" : which == 37 ? "lead8 pace8 depth3" : which == 38 ? "lead8 pace16 depth3" : which == 39 ? "lead8 no pause" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 19 ? "pc (runtime lanes)" : which == 20 ? "pc-r1 (depth 1, no pause)" : which == 21 ? "pace8" : which == 22 ? "pace10" : which == 23 ? "d2-pace8" : which == 24 ? "d2-pace16" : which == 25 ? "d2-pace24" : which == 26 ? "d2-pace32" : which == 30 ? "lead8" : which == 31 ? "lead8+24" : which == 32 ? "lead4+16" : which == 33 ? "lead8+32" : which == 34 ? "lead0 (no graded wait)" : which == 40 ? "pc2 d1 (64u fixed)" : which == 41 ? "pc2 d2" : which == 42 ? "pc2 d2 pace4" : which == 43 ? "pc2 d2 pace8" : which == 44 ? "pc2 d2 pace2" : which == 35 ? "lead8 pace4" : which == 36 ? "lead8 pace12" : which == 37 ? "lead8 pace8 depth3" : which == 38 ? "lead8 pace16 depth3" : which == 39 ? "lead8 no pause" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -1147,6 +1171,13 @@ int main(int argc, char** argv) {
       for (int w : {1, 30, 31, 32, 33}) run_md5(512, 10ull << 20, 7, rep == 0, w);
     for (int w : {1, 30, 31, 32, 33}) run_md5(8192, 1ull << 20, 5, true, w);
     return bad ? 1 : 0;
+  }
+  if (!strcmp(mode, "pc2_pace")) {
+    // the 64 KiB-ring kernel (16 385..32 768 chunks): producer depth and pause
+    for (int rep = 0; rep < 2; ++rep)
+      for (int B : {20480, 32768})
+        for (int w : {5, 40, 41, 42, 43, 44}) run_md5(B, 1ull << 20, 5, rep == 0, w, 4352);
+    return 0;
   }
   if (!strcmp(mode, "lead_pace")) {
     // with the graded wait shipped: producer pause and depth again
