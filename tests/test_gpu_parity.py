@@ -235,12 +235,15 @@ def test_pool_buffers_in_any_order(golden):
     got = qsmd5.hash_batch(chunks)
     assert hexes(got) == [g["md5"][i] for i in order] + [md5_ref(b"").hex()]
 
-    def rate(order):
+    def rate(order):  # best of 3 timed calls after a warm-up: one slow call is noise
         ch = [(t.data_ptr() + i * L, L) for i in order]
         qsmd5.hash_batch(ch)
-        t0 = time.perf_counter()
-        qsmd5.hash_batch(ch)
-        return 1.0 / (time.perf_counter() - t0)
+        best = float("inf")
+        for _ in range(3):
+            t0 = time.perf_counter()
+            qsmd5.hash_batch(ch)
+            best = min(best, time.perf_counter() - t0)
+        return 1.0 / best
     in_order, shuffled = rate(range(n)), rate(perm)
     print("pool order %.1f GiB/s, shuffled %.1f GiB/s" % (in_order * 5, shuffled * 5))
     assert shuffled > 0.93 * in_order, (in_order, shuffled)
