@@ -30,6 +30,15 @@ void compress(uint32_t h[4], const uint8_t* p, uint64_t nblocks);
 
 constexpr uint32_t kIV[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
 
+// Multi-buffer form (md5_cpu_mb.cpp): 16 independent messages per host thread
+// in the lanes of AVX-512 registers, each lane refilled from `pull` when its
+// message ends.  pull(ctx, &i) hands out message i (ptrs[i], lens[i] -> out[i])
+// or returns false when none is left.  Call only if mb16_available().
+typedef bool (*MbPull)(void* ctx, uint32_t* i);
+bool mb16_available();
+void md5_mb16(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16], MbPull pull,
+              void* ctx);
+
 // Streaming state: the MD5 class (update()* then final()), any piece sizes.
 struct Ctx {
   uint32_t h[4] = {kIV[0], kIV[1], kIV[2], kIV[3]};

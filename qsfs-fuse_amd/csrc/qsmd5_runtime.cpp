@@ -1368,12 +1368,42 @@ std::vector<uint32_t> plan_split(const qsmd5_chunk* chunks, size_t n, int flags)
   return idx;
 }
 
+// The multi-buffer queue of cpu_batch: host chunks go to the AVX-512 lanes,
+// device chunks met on the way are hashed by the calling thread right there.
+struct MbQueue {
+  std::atomic<size_t>* next;
+  size_t n;
+  const uint32_t* order;
+  const uint8_t* on_dev;
+  std::atomic<int>* hip_err;
+  bool (*device_chunk)(void* self, uint32_t i);
+  void* self;
+};
+
+bool mb_pull(void* ctx, uint32_t* out) {
+  MbQueue* q = static_cast<MbQueue*>(ctx);
+  for (size_t k; (k = q->next->fetch_add(1)) < q->n && q->hip_err->load() == (int)hipSuccess;) {
+    const uint32_t i = q->order[k];
+    if (!q->on_dev[i]) {
+      *out = i;
+      return true;
+    }
+    if (!q->device_chunk(q->self, i)) return false;
+  }
+  return false;
+}
+
 // The CPU backend: every chunk on up to cpu_threads() host threads (longest
-// first, taken from a shared counter).  A device-resident chunk is read through
+// first, taken from a shared counter).  With AVX-512 (QSMD5_CPU_MB=0: never)
+// and at least 2 host chunks per thread, each thread runs 16 host chunks at
+// once, one per vector lane (md5_cpu_mb.cpp): 7-10x the scalar rate per
+// thread (ubench/cpu_mb_rate.py).  The routing cost model above still prices
+// the scalar path, so a batch is never sent to the CPU on the strength of it.  A device-resident chunk is read through
 // the thread's own 8 MiB host buffer, piece by piece, so a fallback over a large
 // device batch holds at most 8 MiB per thread of host memory; that needs a
 // working HIP context.
-int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags) {
+int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags,
+              bool allow_mb = true) {
   std::vector<uint64_t> len(n);
   uint64_t total = 0;
   for (size_t i = 0; i < n; ++i) {
@@ -1401,20 +1431,27 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return len[a] > len[b]; });
   std::atomic<size_t> next{0};
   std::atomic<int> hip_err{(int)hipSuccess};
-  auto set_err = [&](hipError_t e) {
-    int ok = (int)hipSuccess;
-    hip_err.compare_exchange_strong(ok, (int)e);
-  };
-  auto work = [&]() noexcept {
+  size_t n_host = 0;
+  for (size_t i = 0; i < n; ++i) n_host += !on_dev[i];
+  // A lane's chain runs at ~0.6x a scalar chain (the 16 lanes share the
+  // vector pipes), so the lanes pay once a thread has 2 or more chunks.
+  const bool mb = allow_mb && n_host >= 2 * std::min<size_t>(cpu_threads(), n) &&
+                  env_u64("QSMD5_CPU_MB", 1) && qsmd5::cpu::mb16_available();
+  std::vector<const uint8_t*> ptrs;
+  if (mb) {
+    ptrs.resize(n);
+    for (size_t i = 0; i < n; ++i) ptrs[i] = static_cast<const uint8_t*>(chunks[i].ptr);
+  }
+  struct Worker {
+    const qsmd5_chunk* chunks;
+    const uint64_t* len;
+    uint8_t (*digests)[16];
+    std::atomic<int>* hip_err;
     std::unique_ptr<uint8_t[]> bounce;
-    for (size_t k; (k = next.fetch_add(1)) < n && hip_err.load() == (int)hipSuccess;) {
-      const uint32_t i = order[k];
-      const uint8_t* p = static_cast<const uint8_t*>(chunks[i].ptr);
-      if (!on_dev[i]) {
-        qsmd5::cpu::md5(p, len[i], digests[i]);
-        continue;
-      }
+    // a device chunk through the thread's 8 MiB host buffer; false on a HIP error
+    bool device_chunk(uint32_t i) {
       constexpr uint64_t kPiece = 8ull << 20;
+      const uint8_t* p = static_cast<const uint8_t*>(chunks[i].ptr);
       if (!bounce) bounce.reset(new (std::nothrow) uint8_t[kPiece]);
       if (!bounce) return set_err(hipErrorOutOfMemory);
       qsmd5::cpu::Ctx c;
@@ -1425,6 +1462,30 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
         c.update(bounce.get(), m);
       }
       c.final(digests[i]);
+      return true;
+    }
+    bool set_err(hipError_t e) {
+      int ok = (int)hipSuccess;
+      hip_err->compare_exchange_strong(ok, (int)e);
+      return false;
+    }
+  };
+  auto work = [&]() noexcept {
+    Worker w{chunks, len.data(), digests, &hip_err, nullptr};
+    if (mb) {
+      MbQueue q{&next, n, order.data(), on_dev.data(), &hip_err,
+                [](void* self, uint32_t i) { return static_cast<Worker*>(self)->device_chunk(i); },
+                &w};
+      qsmd5::cpu::md5_mb16(ptrs.data(), len.data(), digests, mb_pull, &q);
+      return;
+    }
+    for (size_t k; (k = next.fetch_add(1)) < n && hip_err.load() == (int)hipSuccess;) {
+      const uint32_t i = order[k];
+      if (!on_dev[i]) {
+        qsmd5::cpu::md5(chunks[i].ptr, len[i], digests[i]);
+        continue;
+      }
+      if (!w.device_chunk(i)) return;
     }
   };
   // Threads only where they pay (a thread start costs ~20-50 us): >= 1 MiB
@@ -1512,7 +1573,9 @@ int run_split(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int g
   std::string cpu_err;
   auto cpu_side = [&]() noexcept {
     try {
-      rc_cpu = cpu_batch(cc.data(), cc.size(), cdig, gflags);
+      // the longest chunks, few per thread: their chains set the time, and a
+      // scalar chain is the faster one (no multi-buffer lanes)
+      rc_cpu = cpu_batch(cc.data(), cc.size(), cdig, gflags, false);
     } catch (...) {
       rc_cpu = fail(-ENOMEM, "qsmd5: CPU share of a split batch failed");
     }

@@ -221,3 +221,33 @@ def test_product_library_does_not_carry_the_oracle():
     assert "oracle_" not in syms and "ref_md5" not in syms
     allsyms = subprocess.run(["nm", so], capture_output=True, text=True).stdout
     assert "oracle_md5" not in allsyms
+
+
+def test_multibuffer_and_scalar_paths_agree():
+    """Both CPU paths against the oracle, each in its own process: the AVX-512
+    multi-buffer lanes (md5_cpu_mb.cpp, when the host has AVX-512F) and the
+    scalar chain (QSMD5_CPU_MB=0).  Ragged lengths 0..3 MiB at odd offsets, so
+    lanes run out at different blocks and are refilled mid-batch, plus tails
+    on every side of the 56-byte padding edge."""
+    script = r'''
+import ctypes, random, sys
+sys.path.insert(0, %r); sys.path.insert(0, %r)
+import qsmd5
+from oracle_util import md5_many
+rng = random.Random(77)
+lens = [rng.choice([0, 1, 55, 56, 63, 64, 65, 119, 120]) for _ in range(40)]
+lens += [rng.randrange(0, 3 << 20) for _ in range(160)]
+buf = ctypes.create_string_buffer(bytes(rng.getrandbits(8) for _ in range(1 << 16)) * 80)
+chunks, pos = [], 3
+for L in lens:
+    chunks.append((ctypes.addressof(buf) + pos, L))
+    pos = (pos + L + 7) %% (len(buf) - (3 << 20) - 8)
+got = qsmd5.hash_batch(chunks, flags=qsmd5.FLAG_CPU_ONLY)
+assert got == md5_many(chunks), "CPU backend digests differ from the oracle"
+print("ok", len(chunks))
+''' % (os.path.join(ROOT, "qsfs-fuse_amd"), os.path.join(ROOT, "tests"))
+    for mb in ("1", "0"):
+        env = dict(os.environ, QSMD5_CPU_MB=mb, QSMD5_CPU_THREADS="3")
+        out = subprocess.run([os.sys.executable, "-c", script], env=env, capture_output=True,
+                             text=True, timeout=300)
+        assert out.returncode == 0 and out.stdout.startswith("ok"), (mb, out.stdout + out.stderr[-2000:])
