@@ -1303,6 +1303,29 @@ uint64_t routed_len(const qsmd5_chunk& c, int flags) {
   return (flags & QSMD5_FLAG_REF_TRUNCATE32) ? (c.len & 0xffffffffull) : c.len;
 }
 
+// Opt-in (QSMD5_ROUTE_LANES=1): price the CPU backend's multi-buffer lanes
+// (cpu_batch, md5_cpu_mb.cpp) for batches that will run on them -- AVX-512F,
+// at least 2 chunks per thread, every chunk in host memory.  Measured on the
+// MI355X box's EPYC 9575F: a lane's chain 0.43 GiB/s, a thread 6.9 GiB/s
+// (profiles/r02_cpu_mb_rate.jsonl); priced a little below.  Off by default: a
+// qsfs daemon keeps its cores, and host batches under ~370 parts of 10 MiB
+// (and BASELINE config 4 from host memory) would otherwise leave the GPU.
+constexpr double kLaneChainGiBs = 0.40;
+constexpr double kLaneThreadGiBs = 6.0;
+
+bool lanes_priced(const qsmd5_chunk* chunks, size_t n, int flags) {
+  if (!env_u64("QSMD5_ROUTE_LANES", 0) || !env_u64("QSMD5_CPU_MB", 1) ||
+      !qsmd5::cpu::mb16_available() || n < 2 * std::min<size_t>(cpu_threads(), n))
+    return false;
+  if ((flags & QSMD5_FLAG_HOST) || qsmd5_device_count() <= 0) return true;
+  Classifier cls(flags, n);
+  for (size_t i = 0; i < n; ++i) {
+    int owner = -1;
+    if (chunks[i].len && cls(chunks[i].ptr, &owner) == kDeviceMem) return false;
+  }
+  return true;
+}
+
 // True when the CPU is expected to finish this batch first (see above).
 bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
   uint64_t total = 0, longest = 0;
@@ -1311,7 +1334,13 @@ bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
     total += L;
     longest = std::max(longest, L);
   }
-  return cpu_est_ms(longest, total) < gpu_est_ms(longest, total);
+  double cpu_ms = cpu_est_ms(longest, total);
+  if (lanes_priced(chunks, n, flags)) {
+    const double GiB = 1073741824.0;
+    cpu_ms = 1e3 * std::max((double)longest / kLaneChainGiBs,
+                            (double)total / ((double)cpu_threads() * kLaneThreadGiBs)) / GiB;
+  }
+  return cpu_ms < gpu_est_ms(longest, total);
 }
 
 // Ragged batches (qsfs -b sweeps, a file's parts plus small files): the GPU's

@@ -26,6 +26,7 @@ from conftest import ROOT
 from oracle_util import lcg_bytes, md5_many
 
 CPU = qsmd5.FLAG_CPU_ONLY
+MiB = 1 << 20
 
 
 def _hex_all(chunks, flags=CPU):
@@ -251,3 +252,24 @@ print("ok", len(chunks))
         out = subprocess.run([os.sys.executable, "-c", script], env=env, capture_output=True,
                              text=True, timeout=300)
         assert out.returncode == 0 and out.stdout.startswith("ok"), (mb, out.stdout + out.stderr[-2000:])
+
+
+def test_lane_priced_routing_is_opt_in(monkeypatch, golden):
+    """QSMD5_ROUTE_LANES=1 prices the multi-buffer lanes for host batches:
+    BASELINE config 4's lengths and 64 x 10 MiB then stay on the CPU, 512 x
+    10 MiB still takes the GPU.  Off (the default) the routing is unchanged."""
+    if "avx512f" not in open("/proc/cpuinfo").read():
+        pytest.skip("host without AVX-512F: the lanes are never priced")
+    G, C, S = qsmd5.BACKEND_GPU, qsmd5.BACKEND_CPU, qsmd5.BACKEND_SPLIT
+    lens = golden("ragged.json")["lengths"]
+    monkeypatch.setenv("QSMD5_CPU_THREADS", "4")
+    monkeypatch.delenv("QSMD5_ROUTE_LANES", raising=False)
+    assert qsmd5.route(lens) == S
+    assert qsmd5.route([10 * MiB] * 64) == G
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "1")
+    assert qsmd5.route(lens) == C
+    assert qsmd5.route([10 * MiB] * 64) == C
+    assert qsmd5.route([10 * MiB] * 512) == G
+    assert qsmd5.route([10 * MiB]) == C  # a lone part: scalar, as before
+    monkeypatch.setenv("QSMD5_CPU_MB", "0")  # no lanes, nothing to price
+    assert qsmd5.route(lens) == S

@@ -1,6 +1,6 @@
 """CPU backend rate, scalar (QSMD5_CPU_MB=0) against the AVX-512 multi-buffer
-path (16 messages per thread), on this host: equal parts at an exact stride and
-a ragged set, 1 and 4 threads, every digest checked against the oracle."""
+path (16 messages per thread), on this host: equal parts at an exact stride,
+a ragged set and BASELINE config 4's 659 lengths (pageable host), 1 and 4 threads, every digest checked against the oracle."""
 import os
 import subprocess
 import sys
@@ -14,10 +14,12 @@ import numpy as np
 import qsmd5
 from oracle_util import md5_many
 rng = np.random.default_rng(1)
+RAGGED = json.load(open(%r))["lengths"]
 out = []
 for name, lens in (("16 x 10 MiB", [10 << 20] * 16), ("64 x 10 MiB", [10 << 20] * 64),
                    ("256 x 1 MiB", [1 << 20] * 256),
-                   ("ragged 200, 8 KiB-16 MiB", [int(x) for x in np.exp(rng.uniform(np.log(8192), np.log(16 << 20), 200))])):
+                   ("ragged 200, 8 KiB-16 MiB", [int(x) for x in np.exp(rng.uniform(np.log(8192), np.log(16 << 20), 200))]),
+                   ("config 4 lengths: 659 chunks, 0 B-64 MiB", RAGGED)):
     offs, pos = [], 0
     for L in lens:
         offs.append(pos); pos += L
@@ -31,7 +33,8 @@ for name, lens in (("16 x 10 MiB", [10 << 20] * 16), ("64 x 10 MiB", [10 << 20] 
         best = min(best, time.perf_counter() - t0)
     out.append({"batch": name, "GiBps": round(sum(lens) / 2**30 / best, 3), "ms": round(best * 1e3, 2), "parity": ok})
 print(json.dumps(out))
-''' % (os.path.join(ROOT, "qsfs-fuse_amd"), os.path.join(ROOT, "tests"))
+''' % (os.path.join(ROOT, "qsfs-fuse_amd"), os.path.join(ROOT, "tests"),
+       os.path.join(ROOT, "tests", "golden", "ragged.json"))
 
 for mb in ("0", "1"):
     for thr in ("1", "4"):
