@@ -244,3 +244,23 @@ def test_split_config4_device_resident(auto, golden):
     assert [d.hex() for d in qsmd5.hash_batch(chunks, flags=qsmd5.FLAG_GPU_ONLY)] == gr["md5"]
     gpu_s = time.perf_counter() - t0
     print("config 4 device-resident: split %.3f s, GPU only %.3f s" % (split_s, gpu_s))
+
+
+def test_lane_priced_routing_keeps_host_batch_on_cpu(auto, monkeypatch):
+    """QSMD5_ROUTE_LANES=1 on the box's host CPU: a ragged host batch (62
+    chunks, 1-16 MiB) stays on the CPU's multi-buffer lanes instead of
+    splitting, and every digest equals the oracle's; without the knob it
+    splits as before."""
+    if "avx512f" not in open("/proc/cpuinfo").read():
+        pytest.skip("host without AVX-512F: the lanes are never priced")
+    monkeypatch.setenv("QSMD5_CPU_THREADS", "1")  # one thread: the scalar model splits
+    lens, _bufs, chunks = _ragged_host(seed=33)
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "1")
+    assert qsmd5.route(lens) == qsmd5.BACKEND_CPU
+    s0 = qsmd5.stats()
+    assert qsmd5.hash_batch(chunks) == md5_many(chunks)
+    assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
+    s1 = qsmd5.stats()
+    assert s1["gpu_batches"] == s0["gpu_batches"] and s1["cpu_chunks"] - s0["cpu_chunks"] == len(lens)
+    monkeypatch.delenv("QSMD5_ROUTE_LANES")
+    assert qsmd5.route(lens) == qsmd5.BACKEND_SPLIT
