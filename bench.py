@@ -146,12 +146,13 @@ def cpu_baseline(host_chunks, gpu_hex, gpu_value):
     return {
         "value": by_threads[best_thr], "unit": "GiB/s", "cores": int(best_thr), "kind": kind,
         "sample": "%s, md5(std::string) form, over the same 10 MiB chunks: %s threads on "
-                  "%s chunks (best of 2 passes after a warm-up); value = all %d logical CPUs "
-                  "on all %d chunks. Host: %s, %s sockets, %s physical cores, %d logical CPUs, "
-                  "cgroup CPU quota %s" % (
+                  "%s chunks (best of 2 passes after a warm-up); value = the best of these, "
+                  "%s threads on %d chunks (cores = that thread count). Host: %s, %s sockets, "
+                  "%s physical cores, %d logical CPUs, cgroup CPU quota %s" % (
                       what, "/".join(by_threads), "/".join(str(samples[t]) for t in by_threads),
-                      nproc, n, topo["cpu_model"], topo["sockets"], topo["physical_cores"],
-                      topo["logical_cpus"], quota if quota is not None else "none"),
+                      best_thr, samples[best_thr], topo["cpu_model"], topo["sockets"],
+                      topo["physical_cores"], topo["logical_cpus"],
+                      quota if quota is not None else "none"),
         "agrees_with_gpu": agree,
         "by_threads": by_threads,
         "by_threads_iostream": by_threads_iostream,
@@ -191,6 +192,111 @@ def _traffic_from_profiles():
     return found
 
 
+def _host_mem_available():
+    """Bytes of host memory this node can still give (MemAvailable, capped by
+    the cgroup limit), or None."""
+    avail = None
+    try:
+        for line in open("/proc/meminfo"):
+            if line.startswith("MemAvailable:"):
+                avail = int(line.split()[1]) * 1024
+    except (OSError, ValueError):
+        pass
+    try:
+        cap = open("/sys/fs/cgroup/memory.max").read().strip()
+        if cap != "max":
+            used = int(open("/sys/fs/cgroup/memory.current").read().strip())
+            left = int(cap) - used
+            avail = left if avail is None else min(avail, left)
+    except (OSError, ValueError):
+        pass
+    return avail
+
+
+def config5_host_leg(args, rank, world, dev, cpu=False):
+    """BASELINE config 5 from host memory, the case that scales with GPUs
+    (SURVEY.md §8e): ONE object of 10 000 x 10 MiB parts,
+    part p = LCG(12345 + p).  Rank r holds its contiguous part range
+    shard_range(n, r, world) in its own pinned host memory and hashes it with
+    qsmd5_hash_batch_ex(QSMD5_FLAG_HOST) over its own GPU's PCIe link; the
+    16-byte digests are all-gathered (RCCL) inside the timed region.  Strong
+    scaling: the object is fixed, so value = object bytes / max-over-ranks
+    time.  The reference hashes the same parts one after another on one core
+    (QSTransferManager.cpp:602-673, File.cpp:639-644).
+
+    The object is 97.7 GiB of host memory on the node; when the node has less
+    than 1/0.6 of that free, the part count is cut to fit and the line says so.
+    """
+    import torch
+    import torch.distributed as dist
+    from bench_config5 import HostShard, L as PART
+    from qsmd5.parallel import shard_range
+
+    dist_on = dist.is_initialized()
+    want = args.config5_parts
+    n = want
+    if dist_on:
+        dist.barrier()  # every rank reads free memory before any allocates
+    avail = _host_mem_available()
+    if avail is not None:
+        local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        nodes = max(1, world // max(1, local_world))
+        fit = int(avail * 0.6) // PART * nodes
+        n = max(world, min(want, fit))
+    if dist_on:
+        t = torch.tensor([n], dtype=torch.int64, device="cpu" if cpu or
+                         dist.get_backend() == "gloo" else dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        n = int(t.item())
+    shard = HostShard(n, rank, world, dev, cpu_rehearsal=cpu)
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
+    for _ in range(args.config5_warmup):
+        shard.step()
+    reps = max(1, args.config5_reps)
+    if dist_on:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    table = None
+    for _ in range(reps):
+        table = shard.step()
+    sync()
+    if dist_on:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        tt = torch.tensor([elapsed], dtype=torch.float64,
+                          device="cpu" if cpu or dist.get_backend() == "gloo" else dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    shard.close()
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_10MiB.json")))["md5"]
+    got = [bytes(r).hex() for r in table.cpu().numpy()]
+    ok = n <= len(gold) and got == gold[:n]
+    per_pass = elapsed / reps
+    value = n * PART / float(1 << 30) / per_pass
+    out = {
+        "workload": "BASELINE config 5 from host memory: one object of %d x 10 MiB parts "
+                    "(%.1f GiB), contiguous part range per rank in that rank's pinned host "
+                    "memory, qsmd5_hash_batch_ex(QSMD5_FLAG_HOST) over its own GPU link, "
+                    "16-B digest all-gather inside the timed region" % (n, n * PART / 2.0 ** 30),
+        "value": round(value, 3), "unit": "GiB/s", "scaling": "strong", "n_gpus": world,
+        "parts": n, "parts_per_rank": [shard_range(n, r, world)[1] - shard_range(n, r, world)[0]
+                                       for r in range(world)],
+        "seconds_per_pass": round(per_pass, 4), "passes": reps, "warmup": args.config5_warmup,
+        "per_gpu_GiBps": round(value / world, 3),
+        "collective": ("RCCL all_gather_into_tensor (16 B per part)"
+                       if dist_on and dist.get_backend() == "nccl" else
+                       "gloo all_gather (host)" if dist_on else "none (one rank)"),
+        "path": shard.path,
+        "parity": "ok: %d/%d digests == reference golden" % (n, n) if ok else "FAIL",
+    }
+    if n != want:
+        out["reduced_from"] = want
+        out["reduced_because"] = "node host memory: %.1f GiB free" % ((avail or 0) / 2.0 ** 30)
+    return out, ok
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -203,7 +309,18 @@ def main():
                          "(exercises the RCCL path on a 1-GPU box)")
     ap.add_argument("--rehearse-gloo", action="store_true",
                     help="N>1 rehearsal on a 1-GPU box: every rank on cuda:0, gloo digest gather")
+    ap.add_argument("--config5-parts", type=int, default=10000,
+                    help="parts of the config5_host object (10 MiB each; default the 100 GB object)")
+    ap.add_argument("--config5-reps", type=int, default=3, help="timed passes of config5_host")
+    ap.add_argument("--config5-warmup", type=int, default=1, help="untimed passes of config5_host")
+    ap.add_argument("--no-config5", action="store_true", help="skip the config5_host key")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="no GPU: run only the config5_host leg on CPU ranks over gloo (numpy "
+                         "parts, libqsmd5's CPU backend) and print its JSON line")
     args = ap.parse_args()
+
+    if args.cpu_rehearsal:
+        return cpu_rehearsal(args)
 
     # The bench measures the gfx950 kernels only: no CPU routing or fallback.
     os.environ["QSMD5_BACKEND"] = "gpu"
@@ -355,11 +472,37 @@ def main():
         if not cb["agrees_with_gpu"]:
             result["parity"] = "FAIL (cpu reference disagrees)"
         del host
+    del data, desc, dig, out, table
+    torch.cuda.empty_cache()
+    c5_ok = True
+    if not args.no_config5:
+        # the host-resident object, strong-scaled over the ranks (extra key; the
+        # headline above is unchanged)
+        result["config5_host"], c5_ok = config5_host_leg(args, rank, world, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if distributed:
         dist.destroy_process_group()
-    return 0 if parity_ok else 3
+    return 0 if parity_ok and c5_ok else 3
+
+
+def cpu_rehearsal(args):
+    """The config5_host leg on CPU ranks over gloo (tests/test_bench_gloo.py):
+    sharding, the digest gather, max-over-ranks timing and parity without a GPU."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29517")
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c5, ok = config5_host_leg(args, rank, world, torch.device("cpu"), cpu=True)
+    if rank == 0:
+        print(json.dumps({"rehearsal": "cpu ranks over gloo, libqsmd5 CPU backend (no GPU; not "
+                                       "a measurement)", "n_gpus": world, "config5_host": c5}),
+              flush=True)
+    dist.destroy_process_group()
+    return 0 if ok else 3
 
 
 if __name__ == "__main__":

@@ -89,7 +89,7 @@ def test_bench_two_rank_rehearsal():
     cmd = [PY, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
-           "--batch", "64", "--rehearse-gloo"]
+           "--batch", "64", "--rehearse-gloo", "--config5-parts", "40", "--config5-reps", "1"]
     out = subprocess.run(cmd, env=ENV, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -98,6 +98,8 @@ def test_bench_two_rank_rehearsal():
     assert r["n_gpus"] == 2 and r["config"]["global_batch"] == 128
     assert r["parity"].startswith("ok: 128/128")
     assert r["cpu_baseline"] is None and r["scaling"] == "weak"
+    c5 = r["config5_host"]
+    assert c5["parts_per_rank"] == [20, 20] and c5["parity"] == "ok: 40/40 digests == reference golden"
 
 
 def test_bench_rccl_path_world_one():
@@ -108,7 +110,8 @@ def test_bench_rccl_path_world_one():
     cmd = [PY, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "2", "--warmup", "1",
-           "--batch", "64", "--dist-always", "--no-cpu-baseline"]
+           "--batch", "64", "--dist-always", "--no-cpu-baseline", "--config5-parts", "32",
+           "--config5-reps", "1"]
     out = subprocess.run(cmd, env=ENV, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -116,3 +119,5 @@ def test_bench_rccl_path_world_one():
     r = json.loads(lines[0])
     assert r["n_gpus"] == 1 and r["config"]["global_batch"] == 64
     assert r["parity"].startswith("ok: 64/64")
+    c5 = r["config5_host"]
+    assert c5["collective"].startswith("RCCL") and c5["parity"] == "ok: 32/32 digests == reference golden"
