@@ -41,7 +41,8 @@
  * Lazily initialised: the first call (or qsmd5_init) picks the current HIP
  * device, so it is safe to call after fuse_main() has forked (reference
  * Operations.cpp:1520-1549 initialises threads after the fork for the same
- * reason).
+ * reason).  A child forked AFTER initialisation cannot use the parent's HIP
+ * state: its GPU calls fail with -ENODEV, and auto routing hashes on the CPU.
  *
  * Multi-GPU (one process, e.g. the qsfs daemon): QSMD5_DEVICES="all" or a
  * comma list of ordinals binds several GPUs at init.  qsmd5_hash_batch[_ex]
@@ -104,6 +105,18 @@ typedef struct qsmd5_part {
  * list (idempotent).  Returns 0, -ENODEV when no GPU is usable or the list
  * names a missing GPU, or -EINVAL when the list is malformed. */
 QSMD5_API int qsmd5_init(int flags);
+
+/* Release everything the runtime holds -- each bound GPU's streams, events,
+ * descriptor/digest scratch, staging ring and pinned metadata, and every host
+ * range still registered through qsmd5_register_host -- before static
+ * destructors run (a qsfs daemon's exit path; the reference has no such step:
+ * MD5 holds no global state, MD5.cpp:283).  Waits for a batch in flight on a
+ * GPU to finish.  No other call may start during it, and streaming contexts
+ * must be destroyed first.  Idempotent: 0 when there is nothing to release.
+ * A later call initialises afresh.  In a child forked after initialisation it
+ * drops the parent's handles without a HIP call.  Returns 0, or -EIO if a
+ * HIP release call failed (the resources are dropped either way). */
+QSMD5_API int qsmd5_shutdown(void);
 
 QSMD5_API int qsmd5_abi_version(void);
 
@@ -189,8 +202,9 @@ QSMD5_API int qsmd5_free_pinned(void* ptr);
  * each batch's first touch, and rows in separate registered buffers are
  * gathered by one kernel per column.  The range is widened to
  * whole pages.  Unregister (with the same ptr) before freeing the memory.
- * -EINVAL for a NULL/empty range, a ptr registered twice, or unregistering a
- * ptr this library did not register. */
+ * -EINVAL for a NULL/empty range, a ptr registered twice, a range that
+ * shares a page with one already registered, or unregistering a ptr this
+ * library did not register. */
 QSMD5_API int qsmd5_register_host(void* ptr, size_t bytes);
 QSMD5_API int qsmd5_unregister_host(void* ptr);
 
@@ -200,7 +214,12 @@ QSMD5_API int qsmd5_unregister_host(void* ptr);
  * `min_part`.  Offsets start at `range_begin`.  Writes up to `cap` parts and
  * sets *nparts to the number needed (call with cap = 0 to size).
  * Host-only, needs no GPU.  Reference defaults: buf 10 MiB, min 4 MiB,
- * threshold 20 MiB (configure/Default.cpp:159-177). */
+ * threshold 20 MiB (configure/Default.cpp:159-177).
+ * More than 65 535 parts: -EINVAL, with the count in *nparts and nothing
+ * written.  The reference's part ids are uint16_t (TransferHandle.h:50), so
+ * its part 65 536 gets id 0 and part 65 537 collides with part 1 and is
+ * dropped (TransferHandle.cpp:252-256); part numbers here are the
+ * reference's for every plan it can carry out. */
 QSMD5_API int qsmd5_plan_parts(uint64_t file_size, uint64_t buf_size, uint64_t min_part,
                      uint64_t threshold, uint64_t range_begin, qsmd5_part* parts, size_t cap,
                      size_t* nparts);
@@ -234,14 +253,36 @@ QSMD5_API int qsmd5_last_backend(void);
 
 /* The backend QSMD5_BACKEND=auto picks for this batch while the GPU is
  * healthy: QSMD5_BACKEND_CPU when the CPU's estimated time is the lower
- * (QSMD5_CPU_THREADS threads, default 4, at QSMD5_CPU_GIBS GiB/s each,
- * default 0.7); QSMD5_BACKEND_SPLIT when the batch is ragged enough that
+ * (QSMD5_CPU_THREADS threads, default 4, at this host's measured chain rate
+ * each: qsmd5_get_rates); QSMD5_BACKEND_SPLIT when the batch is ragged enough that
  * handing its longest host chunks to the CPU threads while the GPU hashes the
  * rest cuts the estimate by >= 10% (a device chunk in the CPU share is read
  * back to the host first; QSMD5_SPLIT=0 turns splitting off); else
  * QSMD5_BACKEND_GPU.  A split call counts once in both gpu_batches and
  * cpu_batches of qsmd5_stats. */
 QSMD5_API int qsmd5_route(const qsmd5_chunk* chunks, size_t n, int flags);
+
+/* The rates QSMD5_BACKEND=auto prices a batch with (qsmd5_route), in GiB/s.
+ * They are this host's: the CPU rates are timed once, at the first routing
+ * decision (~1 ms); the GPU chain rate comes from the latest single-launch
+ * GPU batch of <= 16 384 chunks whose longest is >= 4 MiB (0.119 before any).
+ * QSMD5_CPU_GIBS, QSMD5_GPU_CHAIN_GIBS and QSMD5_LINK_GIBS override;
+ * QSMD5_CALIBRATE=0 keeps the built-in CPU defaults. */
+#define QSMD5_RATE_CPU_MEASURED 1   /* cpu_chain_gibs / cpu_lane_thread_gibs timed on this host */
+#define QSMD5_RATE_CPU_ENV 2        /* cpu_chain_gibs from QSMD5_CPU_GIBS */
+#define QSMD5_RATE_GPU_MEASURED 4   /* gpu_chain_gibs from a timed batch */
+#define QSMD5_RATE_GPU_ENV 8        /* gpu_chain_gibs from QSMD5_GPU_CHAIN_GIBS */
+typedef struct qsmd5_rates {
+  double cpu_chain_gibs;       /* one host thread's scalar MD5 chain */
+  double cpu_lane_thread_gibs; /* one host thread's 16 AVX-512 lanes together (0: no AVX-512F) */
+  double gpu_chain_gibs;       /* one chunk's chain on a GPU lane (latency kernel) */
+  double link_gibs;            /* host -> GPU copy */
+  double d2h_gibs;             /* device chunk read back by the CPU backend */
+  double gpu_call_ms;          /* fixed cost of a GPU batch */
+  int cpu_threads;             /* QSMD5_CPU_THREADS (default 4) */
+  int source;                  /* QSMD5_RATE_* bits */
+} qsmd5_rates;
+QSMD5_API int qsmd5_get_rates(qsmd5_rates* out);
 
 /* Process-wide backend counters since load. */
 typedef struct qsmd5_stats {

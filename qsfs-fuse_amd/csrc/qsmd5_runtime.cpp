@@ -20,9 +20,11 @@
 // stride sends every lane's request to the same HBM channel).
 #include <errno.h>
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -177,7 +179,20 @@ Runtime& rt() {
 
 Dev& primary() { return *rt().devs[0]; }
 
-std::once_flag g_init_once;
+// Lazy initialisation, undone by qsmd5_shutdown.  g_init_state: 0 = not yet
+// (or shut down), 1 = ready, 2 = failed (sticky until a shutdown).  The fast
+// path is one acquire load; init and shutdown serialise on g_init_mu.
+std::mutex g_init_mu;
+std::atomic<int> g_init_state{0};
+pid_t g_init_pid = 0;                     // the process that owns the HIP state
+std::atomic<bool> g_forked_child{false};  // set in a child forked after init
+
+void on_fork_child() {
+  // HIP state does not survive fork(): a child of an initialised process
+  // must not touch the parent's streams or buffers (it hashes on the CPU
+  // under auto routing, see ensure_init).
+  if (g_init_state.load() != 0) g_forked_child.store(true);
+}
 
 // Devices to bind: QSMD5_DEVICES = "all" or a comma list of ordinals (an
 // ordinal may repeat: two contexts on one GPU, used by the tests to exercise
@@ -235,6 +250,52 @@ int init_dev(Dev& d, int device) {
   return 0;
 }
 
+// Everything init_dev and run_batch allocated for one GPU: wait for its
+// streams, then destroy events and streams and free scratch, staging and the
+// pinned metadata (qsmd5_shutdown).  Every handle is tried even if one fails.
+int release_dev(Dev& d) {
+  if (d.device < 0) return 0;
+  int bad = 0;
+  auto chk = [&](hipError_t e) {
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      bad = 1;
+    }
+  };
+  chk(hipSetDevice(d.device));
+  for (int k = 0; k < kMaxCopyStreams; ++k)
+    if (d.copy[k]) {
+      chk(hipStreamSynchronize(d.copy[k]));
+      chk(hipStreamDestroy(d.copy[k]));
+      d.copy[k] = nullptr;
+    }
+  for (auto& s : d.compute)
+    if (s) {
+      chk(hipStreamSynchronize(s));
+      chk(hipStreamDestroy(s));
+      s = nullptr;
+    }
+  for (hipEvent_t* e : {&d.ev_meta, &d.ev_first, &d.ev_last})
+    if (*e) {
+      chk(hipEventDestroy(*e));
+      *e = nullptr;
+    }
+  for (DevBuf* b : {&d.d_meta, &d.d_dig, &d.d_staging, &d.d_state})
+    if (b->p) {
+      chk(hipFree(b->p));
+      b->p = nullptr;
+      b->cap = 0;
+    }
+  for (HostPinned* b : {&d.h_meta, &d.h_dig})
+    if (b->p) {
+      chk(hipHostFree(b->p));
+      b->p = nullptr;
+      b->cap = 0;
+    }
+  d.device = -1;
+  return bad;
+}
+
 void do_init() {
   Runtime& r = rt();
   int n = 0;
@@ -252,12 +313,12 @@ void do_init() {
   }
   for (int o : ords) {
     Dev* d = new Dev;
+    r.devs.push_back(d);  // kept even if half built: qsmd5_shutdown releases it
     if (int rc = init_dev(*d, o)) {
       r.init_rc = rc;
       r.init_msg = t_last_error;
-      return;  // partially built Devs are leaked with the runtime: init failed for good
+      return;
     }
-    r.devs.push_back(d);
   }
   r.shard_bytes = env_u64("QSMD5_SHARD_BYTES", 4ull << 30);
   (void)hipSetDevice(r.devs[0]->device);
@@ -266,7 +327,19 @@ void do_init() {
 }
 
 int ensure_init() {
-  std::call_once(g_init_once, do_init);
+  if (g_init_state.load(std::memory_order_acquire) == 0) {
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    if (g_init_state.load() == 0) {
+      static std::once_flag atfork_once;
+      std::call_once(atfork_once, [] { pthread_atfork(nullptr, nullptr, on_fork_child); });
+      g_init_pid = getpid();
+      do_init();
+      g_init_state.store(rt().ready ? 1 : 2, std::memory_order_release);
+    }
+  }
+  if (g_forked_child.load(std::memory_order_relaxed))
+    return fail(-ENODEV, "qsmd5: the GPU runtime was initialised before fork(); a forked child "
+                         "cannot use it (initialise after the fork, as qsfs does)");
   Runtime& r = rt();
   if (!r.ready) return fail(r.init_rc ? r.init_rc : -ENODEV, r.init_msg);
   // Calls may come from threads whose current device differs.
@@ -543,6 +616,22 @@ uint32_t pc_lanes_for(size_t n, uint64_t longest) {
 using qsmd5::kNoColumns;
 using qsmd5::stage_bytes;
 
+// The GPU chain rate of the latest timed batch (double bits; 0 = none yet),
+// for the routing cost model ("backend routing" below).  Only a batch that ran
+// as ONE latency-kernel launch (<= 16 384 chunks, one chain per lane) with a
+// longest chunk of >= 4 MiB measures a chain: its kernel time is that chain's.
+std::atomic<uint64_t> g_gpu_chain_bits{0};
+
+void note_gpu_chain(uint64_t longest, size_t n, unsigned launches, double kernel_ms) {
+  if (launches != 1 || n > qsmd5::kLatencyKernelResident || longest < (4ull << 20) || kernel_ms <= 0)
+    return;
+  const double gibs = (double)longest / (kernel_ms * 1e-3) / 1073741824.0;
+  if (gibs < 0.01 || gibs > 10.0) return;  // not a chain-bound launch
+  uint64_t bits;
+  memcpy(&bits, &gibs, sizeof(bits));
+  g_gpu_chain_bits.store(bits, std::memory_order_relaxed);
+}
+
 // The synchronous batch on one GPU: device chunks in one launch; host chunks
 // staged in slices with copy/compute overlap.  Caller holds r.mu and has made
 // r.device current.  Device chunks must live on r.device: a kernel reading
@@ -769,6 +858,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   const qsmd5_chunk* d_seg = d_desc + n;
   uint32_t* d_dig = static_cast<uint32_t*>(r.d_dig.p);
   bool first_kernel = true;
+  unsigned launches = 0;   // hashing launches (a chain-rate sample needs exactly one)
   size_t gather_next = 0;  // gather rows launched so far (slices take them in order)
   unsigned used = 0;  // compute streams (1..) that ran work: joined into s0 at the end
   auto mark_first = [&](hipStream_t s) -> int {
@@ -781,6 +871,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   auto launch = [&](hipStream_t s, const uint32_t* ord, size_t cnt, bool aligned16,
                     uint64_t longest) -> int {
     if (int rc = mark_first(s)) return rc;
+    ++launches;
     static const uint32_t skew = (uint32_t)env_u64("QSMD5_SKEW_BLOCKS", qsmd5::kPcSkewBlocks);
     hipError_t e = qsmd5::launch_batch(d_desc, ord, (uint32_t)cnt, d_dig,
                                        kernel_choice(cnt, aligned16), s, skew,
@@ -872,6 +963,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     if (trace) QS_HIP(hipEventRecord(tr[4 * si + 2], cs));
     if (g.ncols > 1) {
       if (int rc = mark_first(cs)) return drain(rc);
+      ++launches;
       e = qsmd5::launch_column(d_seg + sl.seg0, d_order + n + sl.seg0, (uint32_t)sl.active, d_dig,
                                col_off, W, static_cast<uint32_t*>(r.d_state.p), cs);
       if (e != hipSuccess) return drain(hip_fail(e, "qsmd5 column kernel launch"));
@@ -925,6 +1017,11 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   float kms = 0;
   r.last_kernel_ms =
       (!first_kernel && hipEventElapsedTime(&kms, r.ev_first, r.ev_last) == hipSuccess) ? kms : 0.0;
+  {
+    uint64_t longest = 0;
+    for (uint64_t L : len) longest = std::max(longest, L);
+    note_gpu_chain(longest, n, launches, r.last_kernel_ms);
+  }
   r.last_wall_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return 0;
@@ -1207,6 +1304,7 @@ int group_commit(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], in
 struct DeviceRestore {
   int prev = -1;
   DeviceRestore() {
+    if (g_forked_child.load(std::memory_order_relaxed)) return;  // not our HIP state
     if (hipGetDevice(&prev) != hipSuccess) {
       prev = -1;
       (void)hipGetLastError();
@@ -1236,20 +1334,32 @@ int guarded(F&& f) {
 // log the backend; an env knob selects auto/cpu/gpu.
 //
 // A GPU batch costs one chain time for its longest chunk whatever its width
-// (the latency kernel's 1207 cycles per 64 B at 2.4 GHz = 0.119 GiB/s per
-// chain), plus its bytes over the host link (53.7 GiB/s measured) and ~30 us
-// of calls.  The CPU hashes each chunk as one chain too, ~6x faster per chain
-// (md5_cpu.h; 0.6-0.8 GiB/s per core), but only T = QSMD5_CPU_THREADS chains
-// at a time.  So a lone part (the reference's unchanged per-part md5() call
-// site, QSClient.cpp:369-371) is always faster on the CPU: 10 MiB in ~14 ms
-// against ~84 ms.  Equal parts of any size break even at
-//   n = (1/r_chain + ...) ~ 8.4 / (1/(T r_cpu) - 1/r_link) ~ 25 parts at T = 4,
-// and 1 KiB objects at ~30 per call.  Above that the gfx950 kernels win, and
-// win by 20-70x on whole files (batch pre-hash, §8f row 1).
-constexpr double kGpuChainGiBs = 0.119;
+// (r_gpu per chain: the latency kernel's ~1190 cycles per 64 B at 2.4 GHz =
+// 0.12 GiB/s), plus its host bytes over the link (53.7 GiB/s measured) and
+// ~30 us of calls.  The CPU hashes each chunk as one chain too, several times
+// faster per chain (r_cpu, md5_cpu.h), but only T = QSMD5_CPU_THREADS chains
+// at a time, and a device-resident chunk must first come back over the link.
+// So a lone part (the reference's unchanged per-part md5() call site,
+// QSClient.cpp:369-371) is always faster on the CPU.  Equal host parts of size
+// S break even at
+//   n* = (S / r_gpu + call) / (S / (T r_cpu) - S / r_link)
+// -- ~25 parts of 10 MiB at T = 4 and r_cpu = 0.7 GiB/s.  Above that the
+// gfx950 kernels win, by 20-70x on whole files (batch pre-hash, §8f row 1).
+//
+// The rates are this host's, not constants: r_cpu is
+// timed once, at the first routing decision, on a 128 KiB buffer (~0.2 ms;
+// best of 3), and so is one thread's 16-lane AVX-512 group when the host has
+// it; r_gpu is taken from the kernel time of the latest single-launch GPU
+// batch of <= 16 384 chunks whose longest chunk is >= 4 MiB (one chain per
+// lane: the regime the estimate describes), and is 0.119 GiB/s until then.
+// QSMD5_CPU_GIBS / QSMD5_GPU_CHAIN_GIBS / QSMD5_LINK_GIBS override them;
+// QSMD5_CALIBRATE=0 keeps the defaults.  qsmd5_get_rates reports what is used.
+constexpr double kGpuChainGiBs = 0.119;  // until a batch has been timed on this GPU
 constexpr double kLinkGiBs = 53.7;
 constexpr double kGpuCallMs = 0.03;
 constexpr double kD2HGiBs = 10.0;  // device chunk read back by the CPU backend (8 MiB pieces)
+constexpr double kCpuChainGiBs = 0.7;  // QSMD5_CALIBRATE=0, or a timer that failed
+constexpr double kGiB = 1073741824.0;
 
 enum Backend { kAuto = 0, kGpu = 1, kCpu = 2 };
 
@@ -1281,22 +1391,105 @@ size_t cpu_threads() {
   return (size_t)std::max<uint64_t>(1, std::min<uint64_t>(hw, env_u64("QSMD5_CPU_THREADS", 4)));
 }
 
-double cpu_gibs_per_thread() {
-  const char* e = getenv("QSMD5_CPU_GIBS");
+double env_gibs(const char* name) {
+  const char* e = getenv(name);
   const double v = e && *e ? atof(e) : 0.0;
-  return v > 0 ? v : 0.7;
+  return v > 0 ? v : 0.0;
 }
 
-// Estimated wall time (ms) of a batch whose longest chunk is `longest` bytes
-// and whose chunks total `total` bytes, on each backend (see above).
-double gpu_est_ms(uint64_t longest, uint64_t total) {
-  const double GiB = 1073741824.0;
-  return kGpuCallMs + 1e3 * ((double)longest / kGpuChainGiBs + (double)total / kLinkGiBs) / GiB;
+// This host's CPU MD5 rates, timed once (see above).
+struct CpuRates {
+  double chain = kCpuChainGiBs;  // one thread, one scalar chain
+  double lane_thread = 0;        // one thread, 16 AVX-512 lanes together (0: no AVX-512F)
+  bool measured = false;
+};
+
+CpuRates measure_cpu_rates() {
+  CpuRates r;
+  if (!env_u64("QSMD5_CALIBRATE", 1)) return r;
+  constexpr size_t kBytes = 128u << 10;
+  std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[kBytes]);
+  if (!buf) return r;
+  for (size_t i = 0; i < kBytes; ++i) buf[i] = (uint8_t)(i * 131u + (i >> 9));
+  auto best_of_3 = [](auto&& f) {
+    double best = 1e30;
+    for (int k = 0; k < 3; ++k) {  // the first pass also wakes an idle core
+      const auto t0 = std::chrono::steady_clock::now();
+      f();
+      best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    }
+    return best;
+  };
+  uint8_t d[16];
+  const double t_chain = best_of_3([&] { qsmd5::cpu::md5(buf.get(), kBytes, d); });
+  if (t_chain > 0) {
+    r.chain = (double)kBytes / t_chain / kGiB;
+    r.measured = true;
+  }
+  if (env_u64("QSMD5_CPU_MB", 1) && qsmd5::cpu::mb16_available()) {
+    // 16 messages of kBytes / 16 (8 KiB), one per lane, run together
+    constexpr uint32_t kLanes = 16;
+    const uint8_t* ptrs[kLanes];
+    uint64_t lens[kLanes];
+    uint8_t out[kLanes][16];
+    for (uint32_t i = 0; i < kLanes; ++i) {
+      ptrs[i] = buf.get() + i * (kBytes / kLanes);
+      lens[i] = kBytes / kLanes;
+    }
+    struct Pull {
+      uint32_t next = 0;
+      static bool take(void* ctx, uint32_t* i) {
+        Pull* p = static_cast<Pull*>(ctx);
+        if (p->next >= kLanes) return false;
+        *i = p->next++;
+        return true;
+      }
+    };
+    const double t_mb = best_of_3([&] {
+      Pull p;
+      qsmd5::cpu::md5_mb16(ptrs, lens, out, Pull::take, &p);
+    });
+    if (t_mb > 0) r.lane_thread = (double)kBytes / t_mb / kGiB;
+  }
+  return r;
 }
-double cpu_est_ms(uint64_t longest, uint64_t total) {
-  const double GiB = 1073741824.0;
+
+const CpuRates& cpu_rates() {
+  static const CpuRates r = measure_cpu_rates();  // thread-safe, once per process
+  return r;
+}
+
+double cpu_gibs_per_thread() {
+  const double v = env_gibs("QSMD5_CPU_GIBS");
+  return v > 0 ? v : cpu_rates().chain;
+}
+
+double gpu_chain_gibs(bool* measured = nullptr) {
+  const double v = env_gibs("QSMD5_GPU_CHAIN_GIBS");
+  if (measured) *measured = false;
+  if (v > 0) return v;
+  const uint64_t bits = g_gpu_chain_bits.load(std::memory_order_relaxed);
+  if (!bits) return kGpuChainGiBs;
+  double g;
+  memcpy(&g, &bits, sizeof(g));
+  if (measured) *measured = true;
+  return g;
+}
+
+double link_gibs() {
+  const double v = env_gibs("QSMD5_LINK_GIBS");
+  return v > 0 ? v : kLinkGiBs;
+}
+
+// Estimated wall time (ms) on each backend of a batch whose longest chunk is
+// `longest` bytes: the GPU moves `host_bytes` over the link, the CPU hashes
+// `total` bytes of which `d2h_bytes` must first be read back from a GPU.
+double gpu_est_ms(uint64_t longest, uint64_t host_bytes) {
+  return kGpuCallMs + 1e3 * ((double)longest / gpu_chain_gibs() + (double)host_bytes / link_gibs()) / kGiB;
+}
+double cpu_est_ms(uint64_t longest, uint64_t total, uint64_t d2h_bytes = 0) {
   const double T = (double)cpu_threads(), rc = cpu_gibs_per_thread();
-  return 1e3 * std::max((double)longest / rc, (double)total / (T * rc)) / GiB;
+  return 1e3 * (std::max((double)longest / rc, (double)total / (T * rc)) + (double)d2h_bytes / kD2HGiBs) / kGiB;
 }
 
 uint64_t routed_len(const qsmd5_chunk& c, int flags) {
@@ -1305,17 +1498,16 @@ uint64_t routed_len(const qsmd5_chunk& c, int flags) {
 
 // Opt-in (QSMD5_ROUTE_LANES=1): price the CPU backend's multi-buffer lanes
 // (cpu_batch, md5_cpu_mb.cpp) for batches that will run on them -- AVX-512F,
-// at least 2 chunks per thread, every chunk in host memory.  Measured on the
-// MI355X box's EPYC 9575F: a lane's chain 0.43 GiB/s, a thread 6.9 GiB/s
-// (profiles/r02_cpu_mb_rate.jsonl); priced a little below.  Off by default: a
-// qsfs daemon keeps its cores, and host batches under ~370 parts of 10 MiB
-// (and BASELINE config 4 from host memory) would otherwise leave the GPU.
-constexpr double kLaneChainGiBs = 0.40;
-constexpr double kLaneThreadGiBs = 6.0;
-
+// at least 2 chunks per thread, every chunk in host memory -- at this host's
+// measured 16-lane rate (a lane's chain = 1/16 of it).  Off by default (DESIGN.md
+// §1): the lanes are faster than the GPU below ~240 parts of 10 MiB at T = 4
+// on the MI355X box's EPYC 9575F (6.9 GiB/s per thread), but they hold T cores
+// at full AVX-512 load for the batch, and a qsfs daemon runs its transfer
+// workers and FUSE threads on those cores; the GPU leaves them free.
 bool lanes_priced(const qsmd5_chunk* chunks, size_t n, int flags) {
   if (!env_u64("QSMD5_ROUTE_LANES", 0) || !env_u64("QSMD5_CPU_MB", 1) ||
-      !qsmd5::cpu::mb16_available() || n < 2 * std::min<size_t>(cpu_threads(), n))
+      !qsmd5::cpu::mb16_available() || n < 2 * std::min<size_t>(cpu_threads(), n) ||
+      cpu_rates().lane_thread <= 0)
     return false;
   if ((flags & QSMD5_FLAG_HOST) || qsmd5_device_count() <= 0) return true;
   Classifier cls(flags, n);
@@ -1326,7 +1518,11 @@ bool lanes_priced(const qsmd5_chunk* chunks, size_t n, int flags) {
   return true;
 }
 
-// True when the CPU is expected to finish this batch first (see above).
+// True when the CPU is expected to finish this batch first (see above).  The
+// estimates first take every chunk as host memory (the GPU's upper bound, the
+// CPU's lower one); only if the CPU still looks faster are the pointers
+// classified, so that device-resident chunks charge the CPU their read-back
+// and the GPU no link time.
 bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
   uint64_t total = 0, longest = 0;
   for (size_t i = 0; i < n; ++i) {
@@ -1334,13 +1530,22 @@ bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
     total += L;
     longest = std::max(longest, L);
   }
-  double cpu_ms = cpu_est_ms(longest, total);
-  if (lanes_priced(chunks, n, flags)) {
-    const double GiB = 1073741824.0;
-    cpu_ms = 1e3 * std::max((double)longest / kLaneChainGiBs,
-                            (double)total / ((double)cpu_threads() * kLaneThreadGiBs)) / GiB;
+  const bool lanes = lanes_priced(chunks, n, flags);  // only for all-host batches
+  auto cpu_ms_of = [&](uint64_t d2h) {
+    if (!lanes) return cpu_est_ms(longest, total, d2h);
+    const double lt = cpu_rates().lane_thread;
+    return 1e3 * std::max((double)longest / (lt / 16.0), (double)total / ((double)cpu_threads() * lt)) / kGiB;
+  };
+  if (!(cpu_ms_of(0) < gpu_est_ms(longest, total))) return false;
+  if (lanes || (flags & QSMD5_FLAG_HOST) || qsmd5_device_count() <= 0) return true;
+  uint64_t dev_bytes = 0;
+  Classifier cls(flags, n);
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t L = routed_len(chunks[i], flags);
+    int owner = -1;
+    if (L && cls(chunks[i].ptr, &owner) == kDeviceMem) dev_bytes += L;
   }
-  return cpu_ms < gpu_est_ms(longest, total);
+  return cpu_ms_of(dev_bytes) < gpu_est_ms(longest, total - dev_bytes);
 }
 
 // Ragged batches (qsfs -b sweeps, a file's parts plus small files): the GPU's
@@ -1363,7 +1568,7 @@ std::vector<uint32_t> plan_split(const qsmd5_chunk* chunks, size_t n, int flags)
   }
   const double gpu_all = gpu_est_ms(longest, total);
   // only where one chain, not the link, sets the GPU's time
-  const double chain_ms = 1e3 * (double)longest / kGpuChainGiBs / 1073741824.0;
+  const double chain_ms = 1e3 * (double)longest / gpu_chain_gibs() / kGiB;
   if (chain_ms < 0.5 * gpu_all) return none;
   const size_t K = std::min<size_t>(n - 1, std::max<size_t>(64, 64 * cpu_threads()));
   std::vector<uint32_t> idx(n);
@@ -1728,9 +1933,57 @@ int qsmd5_init(int flags) {
   return guarded([] { return ensure_init(); });
 }
 
+int qsmd5_shutdown(void) {
+  try {
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    Runtime& r = rt();
+    // In a child forked after init the HIP handles are the parent's: drop
+    // them without a HIP call (the memory goes with the child's exit).
+    const bool own_hip = g_init_pid == getpid() && !g_forked_child.load();
+    int prev = -1;
+    if (own_hip && !r.devs.empty() && hipGetDevice(&prev) != hipSuccess) {
+      prev = -1;
+      (void)hipGetLastError();
+    }
+    int rc = 0;
+    for (Dev* d : r.devs) {
+      {
+        std::lock_guard<std::mutex> dl(d->mu);  // a batch still in flight finishes first
+        if (own_hip && release_dev(*d) != 0 && rc == 0) rc = -EIO;
+      }
+      delete d;
+    }
+    r.devs.clear();
+    {
+      Registry& R = registry();
+      std::lock_guard<std::mutex> rl(R.mu);
+      if (own_hip)
+        for (const auto& kv : R.end_of)
+          if (hipHostUnregister(reinterpret_cast<void*>(kv.first)) != hipSuccess) {
+            (void)hipGetLastError();
+            if (rc == 0) rc = -EIO;
+          }
+      R.base_of.clear();
+      R.end_of.clear();
+    }
+    if (own_hip && prev >= 0) (void)hipSetDevice(prev);
+    r.ready = false;
+    r.init_rc = 0;
+    r.init_msg.clear();
+    r.shard_bytes = 0;
+    g_forked_child.store(false);
+    g_init_state.store(0, std::memory_order_release);
+    if (rc) return fail(rc, "qsmd5_shutdown: a HIP release call failed (resources dropped anyway)");
+    return 0;
+  } catch (...) {
+    return fail(-EIO, "qsmd5: internal error");
+  }
+}
+
 int qsmd5_abi_version(void) { return QSMD5_ABI_VERSION; }
 
 int qsmd5_device_count(void) {
+  if (g_forked_child.load(std::memory_order_relaxed)) return 0;  // the parent's HIP state
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) {
     (void)hipGetLastError();
@@ -1853,8 +2106,13 @@ int qsmd5_register_host(void* ptr, size_t bytes) {
     const uintptr_t lo = u & ~(page - 1), hi = (u + bytes + page - 1) & ~(page - 1);
     Registry& R = registry();
     std::lock_guard<std::mutex> lk(R.mu);
-    if (R.base_of.count(u) || R.end_of.count(lo))
-      return fail(-EINVAL, "qsmd5: range already registered");
+    if (R.base_of.count(u)) return fail(-EINVAL, "qsmd5: range already registered");
+    // Whole pages are registered, so two buffers that share a page cannot both
+    // be: refuse an overlap here instead of a generic hipHostRegister failure.
+    auto it = R.end_of.lower_bound(hi);
+    if (it != R.end_of.begin() && (--it)->second > lo)
+      return fail(-EINVAL, "qsmd5: range shares a page with a range already registered "
+                           "(registration covers whole 4 KiB pages)");
     QS_HIP(hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault));
     R.base_of[u] = lo;
     R.end_of[lo] = hi;
@@ -1879,6 +2137,8 @@ int qsmd5_unregister_host(void* ptr) {
   });
 }
 
+constexpr size_t kMaxRefPartId = 65535;  // uint16_t part ids, TransferHandle.h:50
+
 int qsmd5_plan_parts(uint64_t file_size, uint64_t buf_size, uint64_t min_part, uint64_t threshold,
                      uint64_t range_begin, qsmd5_part* parts, size_t cap, size_t* nparts) {
   if (!nparts) return fail(-EINVAL, "qsmd5: NULL nparts");
@@ -1892,6 +2152,21 @@ int qsmd5_plan_parts(uint64_t file_size, uint64_t buf_size, uint64_t min_part, u
     p.size = sz;
     v.push_back(p);
   };
+  // The reference's part id is uint16_t (Part, TransferHandle.h:50,86; the
+  // PartIdToPartMap key, :45): part 65 536 narrows to id 0, part 65 537 to
+  // id 1, whose map insert then fails (TransferHandle.cpp:252-256) and that
+  // part is silently dropped from the upload.  No numbering can reproduce
+  // such an upload, so a plan of more than 65 535 parts is refused (before it
+  // is built) with the count reported in *nparts.
+  if (file_size >= threshold) {
+    const uint64_t count = file_size / buf_size + (file_size % buf_size ? 1 : 0);
+    if (count > kMaxRefPartId) {
+      *nparts = (size_t)count;
+      return fail(-EINVAL, "qsmd5: " + std::to_string(count) + " parts: the reference numbers "
+                           "parts with uint16_t ids (TransferHandle.h:50), so parts above 65535 "
+                           "would wrap and collide; use a larger buffer size");
+    }
+  }
   try {
     if (file_size < threshold) {
       add(1, 0, file_size);  // single PutObject (QSTransferManager.cpp:543-546)
@@ -1973,6 +2248,27 @@ int qsmd5_route(const qsmd5_chunk* chunks, size_t n, int flags) {
   return guarded([&] {
     if (cpu_is_faster(chunks, n, flags)) return QSMD5_BACKEND_CPU;
     return plan_split(chunks, n, flags).empty() ? QSMD5_BACKEND_GPU : QSMD5_BACKEND_SPLIT;
+  });
+}
+
+int qsmd5_get_rates(qsmd5_rates* out) {
+  if (!out) return fail(-EINVAL, "qsmd5: NULL rates");
+  return guarded([&] {
+    memset(out, 0, sizeof(*out));
+    const CpuRates& c = cpu_rates();
+    const bool cpu_env = env_gibs("QSMD5_CPU_GIBS") > 0;
+    bool gpu_measured = false;
+    out->gpu_chain_gibs = gpu_chain_gibs(&gpu_measured);
+    out->cpu_chain_gibs = cpu_gibs_per_thread();
+    out->cpu_lane_thread_gibs = c.lane_thread;
+    out->link_gibs = link_gibs();
+    out->d2h_gibs = kD2HGiBs;
+    out->gpu_call_ms = kGpuCallMs;
+    out->cpu_threads = (int)cpu_threads();
+    out->source = (c.measured ? QSMD5_RATE_CPU_MEASURED : 0) | (cpu_env ? QSMD5_RATE_CPU_ENV : 0) |
+                  (gpu_measured ? QSMD5_RATE_GPU_MEASURED : 0) |
+                  (env_gibs("QSMD5_GPU_CHAIN_GIBS") > 0 ? QSMD5_RATE_GPU_ENV : 0);
+    return 0;
   });
 }
 

@@ -81,7 +81,7 @@ class BufferSlab {
 // What one wave did: parts hashed, and which backend the library picked.
 struct WaveStats {
   size_t waves = 0, parts = 0;
-  size_t gpu_waves = 0, cpu_waves = 0;
+  size_t gpu_waves = 0, cpu_waves = 0, split_waves = 0;  // by qsmd5_last_backend of each wave
   double gather_s = 0, hash_s = 0, upload_s = 0;  // wall time in each phase
 };
 
@@ -123,7 +123,11 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts,
                   "qsmd5_hash_batch_ex");
     ++st.waves;
     st.parts += n;
-    (qsmd5_last_backend() == QSMD5_BACKEND_GPU ? st.gpu_waves : st.cpu_waves) += 1;
+    switch (qsmd5_last_backend()) {
+      case QSMD5_BACKEND_GPU: ++st.gpu_waves; break;
+      case QSMD5_BACKEND_SPLIT: ++st.split_waves; break;  // longest parts on the CPU, the rest on the GPU
+      default: ++st.cpu_waves; break;
+    }
     const auto t2 = clock::now();
     for (size_t k = 0; k < n; ++k) upload(parts[first + k], pool[k].data, detail::hex(&dig[16 * k]));
     const auto t3 = clock::now();

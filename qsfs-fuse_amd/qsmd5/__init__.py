@@ -20,11 +20,11 @@ import errno
 import os
 
 __all__ = [
-    "Md5Error", "lib", "lib_path", "hexdigest", "md5", "md5_stream", "MD5", "hash_batch",
+    "Md5Error", "lib", "lib_path", "shutdown", "hexdigest", "md5", "md5_stream", "MD5", "hash_batch",
     "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
     "alloc_pinned", "free_pinned", "register_host", "unregister_host", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
     "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST", "FLAG_GPU_ONLY",
-    "FLAG_CPU_ONLY", "stats", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU", "BACKEND_SPLIT",
+    "FLAG_CPU_ONLY", "stats", "rates", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU", "BACKEND_SPLIT",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -54,6 +54,17 @@ class Stats(ctypes.Structure):
 
     def asdict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+class Rates(ctypes.Structure):
+    """qsmd5_rates: what auto routing prices a batch with (GiB/s)."""
+    _fields_ = [("cpu_chain_gibs", ctypes.c_double), ("cpu_lane_thread_gibs", ctypes.c_double),
+                ("gpu_chain_gibs", ctypes.c_double), ("link_gibs", ctypes.c_double),
+                ("d2h_gibs", ctypes.c_double), ("gpu_call_ms", ctypes.c_double),
+                ("cpu_threads", ctypes.c_int), ("source", ctypes.c_int)]
+
+    def asdict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class Part(ctypes.Structure):
@@ -91,6 +102,7 @@ def lib():
     c_u8p = ctypes.POINTER(ctypes.c_uint8)
     sig = {
         "qsmd5_init": (ctypes.c_int, [ctypes.c_int]),
+        "qsmd5_shutdown": (ctypes.c_int, []),
         "qsmd5_abi_version": (ctypes.c_int, []),
         "qsmd5_device_count": (ctypes.c_int, []),
         "qsmd5_strerror": (ctypes.c_char_p, [ctypes.c_int]),
@@ -126,6 +138,7 @@ def lib():
         "qsmd5_last_backend": (ctypes.c_int, []),
         "qsmd5_route": (ctypes.c_int, [ctypes.POINTER(qsmd5_chunk), ctypes.c_size_t, ctypes.c_int]),
         "qsmd5_get_stats": (ctypes.c_int, [ctypes.POINTER(Stats)]),
+        "qsmd5_get_rates": (ctypes.c_int, [ctypes.POINTER(Rates)]),
         "qsmd5_last_timing": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]),
         "qsmd5_synth_fill_lcg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
@@ -157,6 +170,12 @@ def device_count():
     return lib().qsmd5_device_count()
 
 
+def shutdown():
+    """qsmd5_shutdown: release the runtime's GPU resources (idempotent; a later
+    call initialises afresh)."""
+    _check(lib().qsmd5_shutdown(), "qsmd5_shutdown")
+
+
 def kernel_choice(n, flags=0):
     return lib().qsmd5_kernel_choice_ex(n, flags)
 
@@ -176,6 +195,16 @@ def stats():
     st = Stats()
     _check(lib().qsmd5_get_stats(ctypes.byref(st)), "qsmd5_get_stats")
     return st.asdict()
+
+
+RATE_CPU_MEASURED, RATE_CPU_ENV, RATE_GPU_MEASURED, RATE_GPU_ENV = 1, 2, 4, 8
+
+
+def rates():
+    """qsmd5_get_rates as a dict: the rates auto routing uses on this host."""
+    r = Rates()
+    _check(lib().qsmd5_get_rates(ctypes.byref(r)), "qsmd5_get_rates")
+    return r.asdict()
 
 
 def route(lengths, flags=0):

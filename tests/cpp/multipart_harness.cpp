@@ -190,11 +190,11 @@ int main(int argc, char** argv) {
       for (auto& b : pool) qsmd5_unregister_host(b.data);
   }
   printf("{\"size\": %llu, \"parts\": %zu, \"pages\": %zu, \"pool\": %zu, \"pinned\": %s, "
-         "\"slab\": %s, \"registered\": %s, \"register_s\": %.6f, \"waves\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"seconds\": %.6f, "
+         "\"slab\": %s, \"registered\": %s, \"register_s\": %.6f, \"waves\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"split_waves\": %zu, \"seconds\": %.6f, "
          "\"gather_s\": %.6f, \"hash_s\": %.6f, \"upload_s\": %.6f, \"part_sizes\": [",
          (unsigned long long)size, n, file.pages.size(), pool_n, pinned ? "true" : "false",
          slab ? "true" : "false", reg && !pinned ? "true" : "false", register_s, st.waves,
-         st.gpu_waves, st.cpu_waves, total, st.gather_s, st.hash_s, st.upload_s);
+         st.gpu_waves, st.cpu_waves, st.split_waves, total, st.gather_s, st.hash_s, st.upload_s);
   for (size_t i = 0; i < n; ++i) printf("%s%llu", i ? ", " : "", (unsigned long long)parts[i].size);
   printf("], \"hash_s_runs\": [");
   for (size_t i = 0; i < hash_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", hash_runs[i]);

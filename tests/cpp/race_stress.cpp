@@ -12,7 +12,9 @@
 //   - qsmd5_hash_batch / _ex over ragged, unaligned sub-ranges;
 //   - the streaming context (MD5 class) fed in pieces;
 //   - qsmd5_alloc_pinned / qsmd5_free_pinned around a hash;
-//   - qsmd5_hex / qsmd5_base64.
+//   - qsmd5_hex / qsmd5_base64;
+// and, once every thread has returned, qsmd5_shutdown (twice, then a call
+// that re-initialises, then shutdown again) before a normal process exit.
 // Every digest is checked against the CPU oracle (oracle/md5_oracle.c, the
 // checker, linked only into this test).
 // usage: race_stress [threads=6] [rounds=12] [max_len=3145728] [racy]
@@ -21,7 +23,6 @@
 // still reports a race in instrumented code.
 #include <stdint.h>
 #include <stdio.h>
-#include <unistd.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -30,6 +31,12 @@
 #include <vector>
 
 #include "../../include/qsmd5.h"
+
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
+#include <sanitizer/allocator_interface.h>  // __sanitizer_purge_allocator
+#endif
+#endif
 
 extern "C" void oracle_md5(const uint8_t* p, uint64_t len, uint8_t out[16]);
 extern "C" void oracle_lcg_fill(uint8_t* dst, uint64_t len, uint32_t seed);
@@ -189,22 +196,41 @@ int main(int argc, char** argv) {
   std::vector<std::thread> th;
   for (int t = 0; t < T; ++t) th.emplace_back(worker, t, R, L, &ready, T);
   for (auto& x : th) x.join();
+  // The exit path of a qsfs daemon: every thread has returned, so release the
+  // runtime (streams, events, scratch, staging, pinned metadata, registered
+  // ranges) before static destructors run.  Twice (idempotent), then a call
+  // after it must initialise afresh and a second shutdown release that too.
+  int rc = qsmd5_shutdown();
+  if (rc != 0) fail("shutdown", rc, -1, -1);
+  if ((rc = qsmd5_shutdown()) != 0) fail("shutdown (again)", rc, -1, -1);
+  {
+    uint8_t d[16];
+    static const char kAbc[] = "abc";
+    static const uint8_t kWant[16] = {0x90, 0x01, 0x50, 0x98, 0x3c, 0xd2, 0x4f, 0xb0,
+                                      0xd6, 0x96, 0x3f, 0x7d, 0x28, 0xe1, 0x7f, 0x72};
+    if ((rc = qsmd5_hash_one(kAbc, 3, d)) != 0) fail("hash after shutdown", rc, -1, -1);
+    else if (memcmp(d, kWant, 16) != 0) {
+      fprintf(stderr, "MISMATCH hash after shutdown\n");
+      g_bad.fetch_add(1);
+    }
+    if ((rc = qsmd5_shutdown()) != 0) fail("shutdown (after re-init)", rc, -1, -1);
+  }
+#if defined(__has_feature)
+#if __has_feature(address_sanitizer)
+  // ROCm's ASan keeps freed HSA (device and pinned) allocations in its
+  // quarantine.  HIP's own teardown (__cxa_finalize of libamdhip64) shuts HSA
+  // down and then frees host objects; a quarantine recycle at that point
+  // returns a device chunk after the device runtime is gone and ASan's CHECK
+  // (sanitizer_allocator_device.h:125, dev_runtime_unloaded_) aborts the
+  // process (profiles/r02_gpu_suite_asan_teardown.log).  Drain the
+  // quarantine while HSA is still up: the chunks our shutdown just freed are
+  // returned now, not during HIP's teardown.
+  __sanitizer_purge_allocator();
+#endif
+#endif
   printf("race_stress %s: %d threads x %d rounds, %ld digests checked, %d failures\n",
          g_bad.load() ? "FAILED" : "ok", T, R, g_checked.load(), g_bad.load());
   fflush(stdout);
   fflush(stderr);
-  // Leave without running static destructors: the test covers the runtime
-  // while callers race.  The uninstrumented HIP/HSA runtimes' own teardown
-  // (__cxa_finalize of libamdhip64) frees memory that ROCm's ASan device
-  // allocator has already let go of, and its CHECK then fails the process on
-  // some boxes (profiles/r02_gpu_suite_asan_teardown.log) -- after every
-  // digest was checked, inside libhsa-runtime64 frames only.  Only the ASan
-  // build leaves early: under TSan the normal exit joins the runtimes' threads
-  // (an _exit would report them as leaked) and runs TSan's exit-code hook.
-#if defined(__has_feature)
-#if __has_feature(address_sanitizer)
-  _exit(g_bad.load() ? 1 : 0);
-#endif
-#endif
   return g_bad.load() ? 1 : 0;
 }

@@ -25,4 +25,6 @@ def run(args, backend, timeout=300, extra_env=None):
     out = subprocess.run([HARNESS] + list(args), env=env, capture_output=True, text=True,
                          timeout=timeout)
     assert out.returncode == 0, out.stderr[-3000:]
-    return json.loads(out.stdout)
+    r = json.loads(out.stdout)
+    r["_stderr"] = out.stderr
+    return r

@@ -156,6 +156,39 @@ def test_plan_parts_range_begin_and_capacity():
     assert L.qsmd5_plan_parts(5, 0, 0, 0, 0, None, 0, ctypes.byref(need)) == -errno.EINVAL
 
 
+def test_plan_parts_refuses_more_than_uint16_part_ids():
+    """The reference's Part id is uint16_t (TransferHandle.h:50; map key :45):
+    a 70 000-part plan would wrap at part 65 536 and collide with part 1.
+    qsmd5_plan_parts refuses it with -EINVAL and the count; 65 535 parts, the
+    most the reference can number, plan exactly as the restatement says."""
+    L = qsmd5.lib()
+    need = ctypes.c_size_t()
+    total = 70000 * MiB  # 70 000 parts of 1 MiB (qsfs -b 1)
+    rc = L.qsmd5_plan_parts(total, MiB, 4 * MiB, 20 * MiB, 0, None, 0, ctypes.byref(need))
+    assert rc == -errno.EINVAL and need.value == 70000
+    assert b"uint16_t" in L.qsmd5_last_error()
+    with pytest.raises(qsmd5.Md5Error):
+        qsmd5.plan_parts(total, buf_size=MiB)
+    edge = 65535 * MiB
+    got = plan(edge, buf_size=MiB)
+    assert got == prepare_upload_restated(edge, MiB, 4 * MiB, 20 * MiB)
+    assert len(got) == 65535 and got[-1][0] == 65535
+    with pytest.raises(qsmd5.Md5Error):
+        qsmd5.plan_parts(edge + 1, buf_size=MiB)  # 65 536 parts (the averaged tail keeps the id)
+
+
+def test_shutdown_idempotent_without_gpu():
+    """qsmd5_shutdown with nothing to release returns 0, twice; without a GPU
+    an init after it fails with -ENODEV again (the failed state was reset)."""
+    L = qsmd5.lib()
+    assert L.qsmd5_shutdown() == 0
+    assert L.qsmd5_shutdown() == 0
+    if qsmd5.device_count() == 0:
+        assert L.qsmd5_init(0) == -errno.ENODEV
+        assert L.qsmd5_shutdown() == 0
+        assert L.qsmd5_init(0) == -errno.ENODEV
+
+
 def test_kernel_choice_policy_host_only(monkeypatch):
     """The kernel selection is host logic (no GPU): latency kernel up to 16 384
     chunks, its 64 KiB-ring form up to 32 768, then the coalesced kernel for

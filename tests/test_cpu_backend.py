@@ -133,7 +133,9 @@ def test_routing_rule(monkeypatch):
     parts and large object batches go to the GPU; the break-even moves with
     QSMD5_CPU_THREADS as the cost model says."""
     monkeypatch.delenv("QSMD5_CPU_THREADS", raising=False)
-    monkeypatch.delenv("QSMD5_CPU_GIBS", raising=False)
+    # the rule at the reference rates (the host's own rates: the test below)
+    monkeypatch.setenv("QSMD5_CPU_GIBS", "0.7")
+    monkeypatch.setenv("QSMD5_GPU_CHAIN_GIBS", "0.119")
     C, G = qsmd5.BACKEND_CPU, qsmd5.BACKEND_GPU
     MiB = 1 << 20
     for L in (0, 1, 1024, 10 * MiB, 64 * MiB, 4 << 30):
@@ -159,6 +161,65 @@ def test_routing_rule(monkeypatch):
     assert seq == sorted(seq, key=lambda b: b == G)
 
 
+def _predicted_break_even(r, S):
+    """First n for which equal host parts of S bytes go to the GPU, by the cost
+    model of qsmd5_runtime.cpp ("backend routing") at rates r."""
+    GiB = float(1 << 30)
+    T, rc, g, K = r["cpu_threads"], r["cpu_chain_gibs"], r["gpu_chain_gibs"], r["link_gibs"]
+    for n in range(1, 1 << 16):
+        cpu = 1e3 * (max(S / rc, n * S / (T * rc)) + 0.0 / r["d2h_gibs"]) / GiB
+        gpu = r["gpu_call_ms"] + 1e3 * (S / g + n * S / K) / GiB
+        if not cpu < gpu:
+            return n
+    return None
+
+
+def test_routing_prices_this_hosts_measured_rates(monkeypatch):
+    """the CPU rates are timed on this host at the first
+    routing decision (qsmd5_get_rates), and the break-even batch moves exactly
+    as the cost model predicts when the CPU rate is forced slower or faster
+    (QSMD5_CPU_GIBS) or the GPU chain faster (QSMD5_GPU_CHAIN_GIBS)."""
+    for k in ("QSMD5_CPU_GIBS", "QSMD5_GPU_CHAIN_GIBS", "QSMD5_LINK_GIBS", "QSMD5_CPU_THREADS",
+              "QSMD5_ROUTE_LANES"):
+        monkeypatch.delenv(k, raising=False)
+    MiB = 1 << 20
+    r = qsmd5.rates()
+    assert r["source"] & qsmd5.RATE_CPU_MEASURED and not r["source"] & qsmd5.RATE_CPU_ENV
+    assert 0.05 < r["cpu_chain_gibs"] < 10, r
+    if "avx512f" in open("/proc/cpuinfo").read():
+        assert r["cpu_lane_thread_gibs"] > 2 * r["cpu_chain_gibs"], r  # 16 lanes in one thread
+    if qsmd5.device_count() == 0:
+        assert r["gpu_chain_gibs"] == 0.119 and not r["source"] & qsmd5.RATE_GPU_MEASURED
+
+    def break_even(L):
+        lo, hi = 0, 1 << 16
+        while hi - lo > 1:
+            mid = (lo + hi) // 2
+            lo, hi = (mid, hi) if qsmd5.route([L] * mid) == qsmd5.BACKEND_CPU else (lo, mid)
+        return hi
+
+    S = 10 * MiB
+    seen = {}
+    for cpu in (None, "0.35", "0.7", "1.4"):
+        if cpu is None:
+            monkeypatch.delenv("QSMD5_CPU_GIBS", raising=False)
+        else:
+            monkeypatch.setenv("QSMD5_CPU_GIBS", cpu)
+        rr = qsmd5.rates()
+        if cpu is not None:
+            assert rr["cpu_chain_gibs"] == float(cpu) and rr["source"] & qsmd5.RATE_CPU_ENV
+        seen[cpu] = break_even(S)
+        assert seen[cpu] == _predicted_break_even(rr, S), (cpu, rr)
+    assert seen["0.35"] < seen["0.7"] < seen["1.4"]
+    assert (seen["0.35"], seen["0.7"], seen["1.4"]) == (13, 25, 53)  # the worked numbers, DESIGN §1
+    # a faster GPU chain halves the CPU's share
+    monkeypatch.setenv("QSMD5_CPU_GIBS", "0.7")
+    monkeypatch.setenv("QSMD5_GPU_CHAIN_GIBS", "0.238")
+    rr = qsmd5.rates()
+    assert rr["source"] & qsmd5.RATE_GPU_ENV
+    assert break_even(S) == _predicted_break_even(rr, S) < seen["0.7"]
+
+
 def _config4_lengths():
     """BASELINE config 4's shape: 659 chunks, log-uniform 8 KiB-64 MiB."""
     rng = random.Random(7)
@@ -170,7 +231,8 @@ def test_split_routing_rule(monkeypatch):
     the GPU hashes the rest (qsmd5_route -> BACKEND_SPLIT).  Equal parts and
     many small objects never split; QSMD5_SPLIT=0 turns it off."""
     monkeypatch.delenv("QSMD5_CPU_THREADS", raising=False)
-    monkeypatch.delenv("QSMD5_CPU_GIBS", raising=False)
+    monkeypatch.setenv("QSMD5_CPU_GIBS", "0.7")
+    monkeypatch.setenv("QSMD5_GPU_CHAIN_GIBS", "0.119")
     monkeypatch.delenv("QSMD5_SPLIT", raising=False)
     MiB = 1 << 20
     S, G = qsmd5.BACKEND_SPLIT, qsmd5.BACKEND_GPU

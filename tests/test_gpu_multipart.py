@@ -74,3 +74,23 @@ def test_registered_pageable_pool(gold):
     print("512 x 10 MiB, 512 registered pageable buffers: register %.3f s once; hash first pass "
           "%.3f s (%.1f GiB/s), reused %.3f s (%.1f GiB/s)"
           % (r["register_s"], first, 5.0 / first, warm, 5.0 / warm))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pool_kind", ["pinned", "register"])
+def test_pool_refilled_between_waves(gold, pool_kind):
+    """qsfs refills the same transfer buffers for every wave.  A pool of 64
+    buffers for 128 parts: each buffer is filled with part k, hashed through
+    the gather kernel (it reads pinned / registered host memory over PCIe via
+    device pointers), then refilled with part k + 64 and read again.  Stale
+    host data served from a GPU-side cache would repeat wave 1's digests in
+    wave 2; every digest must be part k's own."""
+    flag = "--pinned" if pool_kind == "pinned" else "--register"
+    r = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=64", flag, "--repeat=2"], "gpu",
+            extra_env={"QSMD5_TRACE": "1"})
+    assert r["parts"] == 128 and r["waves"] == 2 and r["gpu_waves"] == 2
+    assert r["md5"] == gold[:128]
+    assert len(set(r["md5"])) == 128  # no wave-2 digest repeats a wave-1 one
+    gathered = [int(ln.split(" regions, ")[1].split()[0]) for ln in r["_stderr"].splitlines()
+                if ln.startswith("qsmd5 trace:") and "gathered rows" in ln]
+    assert len(gathered) == 4 and min(gathered) >= 64, gathered  # 2 passes x 2 waves, every row

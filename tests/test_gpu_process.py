@@ -46,6 +46,60 @@ print("child_ok=%s parent_ok=%s" % (child_ok, parent_ok))
 sys.exit(0 if child_ok and parent_ok else 1)
 '''
 
+SHUTDOWN_SCRIPT = r'''
+import ctypes, hashlib, os, sys
+import qsmd5
+buf = bytearray(os.urandom((3 << 20) + 5))
+view = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
+addr = ctypes.addressof(view)
+want = [hashlib.md5(bytes(buf)).digest(), hashlib.md5(bytes(buf[7:1000007])).digest()]
+chunks = [(addr, len(buf)), (addr + 7, 1000000)]
+for cycle in range(3):
+    qsmd5.register_host(addr, len(buf))          # (re)initialises the runtime
+    p = qsmd5.alloc_pinned(1 << 20)
+    ctypes.memmove(p, addr, 1 << 20)
+    got = qsmd5.hash_batch(chunks + [(p, 1 << 20)])
+    assert got[:2] == want and got[2] == hashlib.md5(bytes(buf[:1 << 20])).digest(), cycle
+    qsmd5.free_pinned(p)
+    if cycle == 2:
+        qsmd5.unregister_host(addr)              # the caller's own unregister, then
+    qsmd5.shutdown()                             # shutdown releases what is left
+    qsmd5.shutdown()                             # idempotent
+st = qsmd5.stats()
+assert st["cpu_batches"] == 0 and st["gpu_batches"] == 3, st
+print("shutdown cycles ok")
+'''
+
+FORK_AFTER_INIT_SCRIPT = r'''
+import os, sys, signal
+import qsmd5
+L = qsmd5.lib()
+assert L.qsmd5_init(0) == 0                       # parent initialised the GPU runtime
+assert qsmd5.hash_batch([b"abc"], flags=qsmd5.FLAG_GPU_ONLY)[0].hex() == "900150983cd24fb0d6963f7d28e17f72"
+pid = os.fork()
+if pid == 0:   # must not touch the parent's HIP state
+    signal.alarm(60)
+    try:
+        ok = L.qsmd5_init(0) == qsmd5.ENODEV
+        try:
+            qsmd5.hash_batch([b"abc"], flags=qsmd5.FLAG_GPU_ONLY)
+            ok = False
+        except qsmd5.Md5Error as e:
+            ok = ok and e.code == qsmd5.ENODEV
+        ok = ok and qsmd5.md5("message digest") == "f96b697d7cb7938d525a2f31aaf161d0"
+        ok = ok and qsmd5.last_backend() == qsmd5.BACKEND_CPU and qsmd5.device_count() == 0
+        ok = ok and L.qsmd5_shutdown() == 0       # drops the handles without a HIP call
+    except Exception as e:
+        print("child error", e, file=sys.stderr)
+        ok = False
+    os._exit(0 if ok else 3)
+_, st = os.waitpid(pid, 0)
+child_ok = os.WIFEXITED(st) and os.WEXITSTATUS(st) == 0
+parent_ok = qsmd5.hash_batch([b"a"], flags=qsmd5.FLAG_GPU_ONLY)[0].hex() == "0cc175b9c0f1b6a831c399e269772661"
+print("child_ok=%s parent_ok=%s" % (child_ok, parent_ok))
+sys.exit(0 if child_ok and parent_ok else 1)
+'''
+
 WORKER_SCRIPT = r'''
 import sys, ctypes
 import qsmd5
@@ -72,6 +126,34 @@ def _free_port():
 def test_init_after_fork():
     out = subprocess.run([PY, "-c", FORK_SCRIPT], env=ENV, capture_output=True, text=True,
                          timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "child_ok=True parent_ok=True" in out.stdout
+
+
+@pytest.mark.parametrize("devices", ["", "0,0"])
+def test_shutdown_releases_and_reinitialises(devices):
+    """qsmd5_shutdown (a daemon's exit path): three cycles of register a
+    pageable buffer + pinned pool + batch + shutdown; each later call
+    re-initialises, a registration released by shutdown can be made again,
+    and every digest matches hashlib.  "0,0" binds two contexts to the GPU."""
+    env = dict(ENV)
+    env.pop("QSMD5_DEVICES", None)
+    if devices:
+        env["QSMD5_DEVICES"] = devices
+    out = subprocess.run([PY, "-c", SHUTDOWN_SCRIPT], env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "shutdown cycles ok" in out.stdout
+
+
+@pytest.mark.cpu_backend
+def test_fork_after_init_child_hashes_on_cpu():
+    """A child forked after the runtime initialised cannot use the parent's
+    HIP state: init and a GPU-only batch fail with -ENODEV without a HIP
+    call, auto routing hashes on the CPU, and the parent keeps its GPU."""
+    env = dict(ENV, QSMD5_BACKEND="auto")
+    out = subprocess.run([PY, "-c", FORK_AFTER_INIT_SCRIPT], env=env, capture_output=True,
+                         text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "child_ok=True parent_ok=True" in out.stdout
 

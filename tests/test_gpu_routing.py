@@ -8,6 +8,7 @@ are injected with QSMD5_INJECT_GPU_FAULT (no real fault is provoked on the
 box).  Every digest is checked against the oracle.
 """
 import ctypes
+import json
 import os
 import statistics
 import subprocess
@@ -264,3 +265,41 @@ def test_lane_priced_routing_keeps_host_batch_on_cpu(auto, monkeypatch):
     assert s1["gpu_batches"] == s0["gpu_batches"] and s1["cpu_chunks"] - s0["cpu_chunks"] == len(lens)
     monkeypatch.delenv("QSMD5_ROUTE_LANES")
     assert qsmd5.route(lens) == qsmd5.BACKEND_SPLIT
+
+
+def test_device_chunks_pay_their_read_back_in_routing(auto):
+    """a device-resident chunk priced for the CPU carries its D2H
+    read-back, and costs the GPU no link time.  n equal 10 MiB chunks where
+    the model (at this host's measured rates, qsmd5_get_rates) sends host
+    memory to the CPU but device memory to the GPU: qsmd5_route agrees with
+    real pointers, and the device batch then runs on the gfx950 kernels."""
+    GiB = float(1 << 30)
+    S = 10 * MiB
+    r = qsmd5.rates()
+    T, rc, g, K, D = (r["cpu_threads"], r["cpu_chain_gibs"], r["gpu_chain_gibs"], r["link_gibs"],
+                      r["d2h_gibs"])
+
+    def cpu_ms(n, dev):
+        return 1e3 * (max(S / rc, n * S / (T * rc)) + (n * S / D if dev else 0)) / GiB
+
+    def gpu_ms(n, dev):
+        return r["gpu_call_ms"] + 1e3 * (S / g + (0 if dev else n * S / K)) / GiB
+
+    ns = [n for n in range(2, 200) if cpu_ms(n, False) < gpu_ms(n, False) and
+          not cpu_ms(n, True) < gpu_ms(n, True)]
+    if not ns:
+        pytest.skip("no batch size separates host from device at these rates: %s" % r)
+    n = ns[len(ns) // 2]
+    dev = torch.empty(n * S, dtype=torch.uint8, device="cuda")
+    qsmd5.synth_fill_lcg(dev.data_ptr(), S, S, 12345, n, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    arr = (qsmd5.qsmd5_chunk * n)()
+    for i in range(n):
+        arr[i].ptr, arr[i].len = dev.data_ptr() + i * S, S
+    assert qsmd5.lib().qsmd5_route(arr, n, 0) == qsmd5.BACKEND_GPU, (n, r)
+    assert qsmd5.route([S] * n) == qsmd5.BACKEND_CPU, (n, r)  # the same sizes as host memory
+    got = qsmd5.hash_batch([(dev.data_ptr() + i * S, S) for i in range(n)])
+    assert qsmd5.last_backend() == qsmd5.BACKEND_GPU
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_10MiB.json")))["md5"]
+    assert [d.hex() for d in got] == gold[:n]
+    print("n=%d device 10 MiB chunks: GPU; as host memory: CPU; rates %s" % (n, r))

@@ -216,3 +216,26 @@ def test_gather_from_registered_pageable_buffers(pinned):
     finally:
         for b in bufs:
             qsmd5.unregister_host(b.ctypes.data)
+
+
+def test_register_refuses_a_shared_page():
+    """Registration covers whole 4 KiB pages: a second buffer in
+    a page already registered is refused with -EINVAL and a clear message,
+    not a generic hipHostRegister failure; after the first is unregistered it
+    can be registered."""
+    import errno
+    blk = np.zeros(4 * 4096, dtype=np.uint8)
+    base = (blk.ctypes.data + 4095) & ~4095
+    a, b = base + 100, base + 4096 + 2000  # a's range ends inside b's page
+    qsmd5.register_host(a, 4096 + 100)
+    try:
+        with pytest.raises(qsmd5.Md5Error) as e:
+            qsmd5.register_host(b, 512)
+        assert e.value.code == -errno.EINVAL and "shares a page" in str(e.value)
+        with pytest.raises(qsmd5.Md5Error) as e:
+            qsmd5.register_host(a, 16)  # the same pointer twice
+        assert e.value.code == -errno.EINVAL
+    finally:
+        qsmd5.unregister_host(a)
+    qsmd5.register_host(b, 512)
+    qsmd5.unregister_host(b)
