@@ -436,8 +436,12 @@ constexpr uint32_t kSkewMinBlocks = 1u << 19;
 // total, [1020] chain waiting at the phase barriers, [1021] chain total,
 // [1022] producer waiting at the barriers, [1023] producer writing the ring
 // (including its wait for the loads).
+// kProbe (ubench attribution only; 0 in every shipped kernel): bit 0 = the
+// producer skips its ring writes, bit 1 = it skips its global loads.  The
+// digests are then wrong; the chain's cycles say what the producer's LDS
+// writes and HBM loads cost it (profiles/r03_attrib.log).
 template <bool kColumn, int kDepth = 1, int kHalf = kPcHalf, bool kNT = false, bool kTrace = false,
-          int kPace = 0, int kGap = 0, int kLead = kPcLead, int kLead2 = 0>
+          int kPace = 0, int kGap = 0, int kLead = kPcLead, int kLead2 = 0, int kProbe = 0>
 __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
                                         const uint32_t* __restrict__ order, uint32_t n,
                                         uint32_t* __restrict__ digests, uint64_t col_off,
@@ -486,7 +490,14 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
     // q % kDepth and are written to the ring kDepth phases after they were
     // issued, so a load has kDepth phases (~2 us each) to land.
     PcBlockRegs r[kDepth][kHalf];
+    if constexpr ((kProbe & 2) != 0) {
+#pragma unroll
+      for (int k = 0; k < kDepth; ++k)
+#pragma unroll
+        for (int h = 0; h < kHalf; ++h) r[k][h] = PcBlockRegs{{lane, lane, lane, lane}, lane};
+    }
     auto load_phase = [&](PcBlockRegs (&rs)[kHalf], uint32_t p) {
+      if constexpr ((kProbe & 2) != 0) return;
       if (nblk) {
 #pragma unroll
         for (int h = 0; h < kHalf; ++h) {
@@ -502,7 +513,7 @@ __device__ __forceinline__ void pc_body(const ChunkDesc* __restrict__ chunks,
           if constexpr (kGap > 0) {
             if (h) __builtin_amdgcn_s_sleep(kGap);
           }
-          pc_write_mk(ring[(p & 1u) * kHalf + h], lane, rs[h], off);
+          if constexpr ((kProbe & 1) == 0) pc_write_mk(ring[(p & 1u) * kHalf + h], lane, rs[h], off);
         }
       }
     };

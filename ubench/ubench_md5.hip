@@ -56,6 +56,16 @@ __global__ __launch_bounds__(128) void k_pc_trace(const ChunkDesc* __restrict__ 
                                                           lanes);
 }
 
+// The shipped 64-lane latency kernel with parts of its producer switched off
+// (pc_body kProbe): what the producer's ring writes and HBM loads cost the chain.
+template <int kProbe>
+__global__ __launch_bounds__(128) void k_pc_probe(const ChunkDesc* __restrict__ c,
+                                                  const uint32_t* __restrict__ o, uint32_t n,
+                                                  uint32_t* __restrict__ d, uint32_t skew) {
+  pc_body<false, kPcDepth, kPcHalf, false, false, kPcPace, 0, kPcLead, 0, kProbe>(
+      c, o, n, d, 0, ~0ull, nullptr, skew, nullptr, 64u);
+}
+
 // chain_phase with the 16 LDS reads of block h+1 spread through block h's 256
 // VALU (one read per kR VALU, placed with sched_group_barrier) instead of
 // issued together at the block's start.
@@ -466,6 +476,15 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
     else if (which == 33)
       hipLaunchKernelGGL((k_pc_lead<8, 32>), dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
+    else if (which == 50)
+      hipLaunchKernelGGL(k_pc_probe<1>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 51)
+      hipLaunchKernelGGL(k_pc_probe<2>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
+    else if (which == 52)
+      hipLaunchKernelGGL(k_pc_probe<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
+                         d_dig, g_skew);
     else
       hipLaunchKernelGGL(k_pc_depth<3>, dim3(grid), dim3(128), 0, 0, d_desc, nullptr, (uint32_t)B,
                          d_dig, g_skew);
@@ -493,7 +512,7 @@ static void run_md5(int B, uint64_t L, int reps, bool check, int which = 0, uint
   if (g_host_pinned) printf("[pinned host, zero-copy] ");
   printf("md5[%s] B=%d L=%llu: median %.3f ms best %.3f ms -> %.2f GiB/s total, r1=%.4f GiB/s/chain, "
          "%.1f cycles/block @2.4GHz\n",
-         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 19 ? "pc (runtime lanes)" : which == 20 ? "pc-r1 (depth 1, no pause)" : which == 21 ? "pace8" : which == 22 ? "pace10" : which == 23 ? "d2-pace8" : which == 24 ? "d2-pace16" : which == 25 ? "d2-pace24" : which == 26 ? "d2-pace32" : which == 30 ? "lead8" : which == 31 ? "lead8+24" : which == 32 ? "lead4+16" : which == 33 ? "lead8+32" : which == 34 ? "lead0 (no graded wait)" : which == 40 ? "pc2 d1 (64u fixed)" : which == 41 ? "pc2 d2" : which == 42 ? "pc2 d2 pace4" : which == 43 ? "pc2 d2 pace8" : which == 44 ? "pc2 d2 pace2" : which == 35 ? "lead8 pace4" : which == 36 ? "lead8 pace12" : which == 37 ? "lead8 pace8 depth3" : which == 38 ? "lead8 pace16 depth3" : which == 39 ? "lead8 no pause" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
+         which == 0 ? "v1" : which == 1 ? "pc" : which == 2 ? "coal" : which == 3 ? "pc-d2" : which == 5 ? "pc-h2" : which == 6 ? "coal-imm" : which == 19 ? "pc (runtime lanes)" : which == 20 ? "pc-r1 (depth 1, no pause)" : which == 21 ? "pace8" : which == 22 ? "pace10" : which == 23 ? "d2-pace8" : which == 24 ? "d2-pace16" : which == 25 ? "d2-pace24" : which == 26 ? "d2-pace32" : which == 30 ? "lead8" : which == 31 ? "lead8+24" : which == 32 ? "lead4+16" : which == 33 ? "lead8+32" : which == 34 ? "lead0 (no graded wait)" : which == 40 ? "pc2 d1 (64u fixed)" : which == 41 ? "pc2 d2" : which == 42 ? "pc2 d2 pace4" : which == 43 ? "pc2 d2 pace8" : which == 44 ? "pc2 d2 pace2" : which == 35 ? "lead8 pace4" : which == 36 ? "lead8 pace12" : which == 37 ? "lead8 pace8 depth3" : which == 38 ? "lead8 pace16 depth3" : which == 39 ? "lead8 no pause" : which == 50 ? "probe: producer writes no ring" : which == 51 ? "probe: producer loads nothing" : which == 52 ? "probe: producer neither loads nor writes" : "pc-d3", B, (unsigned long long)L, med, best, gib / (med / 1e3), (double)L / (1u << 30) / (med / 1e3),
          (med / 1e3) * 2.4e9 / (double)(L / 64));
   if (check) {
     std::vector<uint32_t> dig(4 * (size_t)B);
@@ -1185,6 +1204,18 @@ int main(int argc, char** argv) {
       for (int w : {1, 35, 36, 37, 38, 39}) run_md5(512, 10ull << 20, 7, rep == 0, w);
     for (int w : {1, 37, 38}) run_md5(8192, 1ull << 20, 5, true, w);
     return 0;
+  }
+  if (!strcmp(mode, "attrib")) {
+    // where the chain's last ~55 cycles per block go.  The
+    // shipped kernel (1) against itself with the producer's ring writes (50),
+    // its HBM loads (51) or both (52) switched off; 50-52 hash garbage, so only
+    // the shipped kernel is checked.  (Round 3 also tried an unconditional
+    // producer loop with exact vmcnt waits and an unconditional 17th-dword
+    // load: both slower, profiles/r03_attrib2.log, r03_attrib3.log.)
+    int bad = run_edges(1);
+    for (int rep = 0; rep < 3; ++rep)
+      for (int w : {1, 50, 51, 52}) run_md5(512, 10ull << 20, 5, rep == 0 && w == 1, w);
+    return bad ? 1 : 0;
   }
   if (!strcmp(mode, "chaincost")) {
     // cycles per 64-B block of the chain wave, by what it does besides the steps
