@@ -273,7 +273,7 @@ __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*rin
     static_assert(kLead % 4 == 0 && kLead < 64, "kLead: whole ds_read_b128 groups");
     // block 0 with a graded wait; blocks 1.. below as usual
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_waitcnt(kLgkmcnt0 & ~(0xF << 8) | ((16 - kLead / 4) << 8));
+    __builtin_amdgcn_s_waitcnt((kLgkmcnt0 & ~(0xF << 8)) | ((16 - kLead / 4) << 8));
     __builtin_amdgcn_sched_barrier(0);
     const bool run0 = kAllLive || blk0 < nblk;
     uint32_t mk[64];
@@ -284,7 +284,7 @@ __device__ __forceinline__ void chain_phase(uint32_t (&st)[4], const u32x4 (*rin
     if constexpr (kLead2 > kLead) {
       static_assert(kLead2 % 4 == 0 && kLead2 < 64, "kLead2: whole ds_read_b128 groups");
       __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_waitcnt(kLgkmcnt0 & ~(0xF << 8) | ((16 - kLead2 / 4) << 8));
+      __builtin_amdgcn_s_waitcnt((kLgkmcnt0 & ~(0xF << 8)) | ((16 - kLead2 / 4) << 8));
       __builtin_amdgcn_sched_barrier(0);
       if (run0) md5_steps_mk<kLead, kLead2>(v, mk);
     }
