@@ -16,7 +16,7 @@ export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/bench" -o bench -- \
   python3 "$R/bench.py" > "$OUT/bench.json" 2> "$OUT/bench.err"
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_bench" -o pmc -- \
-  python3 "$R/bench.py" --no-cpu-baseline --steps 2 --warmup 1 > "$OUT/pmc_bench.json" 2> "$OUT/pmc_bench.err"
+  python3 "$R/bench.py" --no-cpu-baseline --no-config5 --steps 2 --warmup 1 > "$OUT/pmc_bench.json" 2> "$OUT/pmc_bench.err"
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_calib" -o pmc -- \
   "$R/ubench/ubench_md5" calib > "$OUT/pmc_calib.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/sat" -o sat -- \
