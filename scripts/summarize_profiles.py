@@ -50,8 +50,8 @@ def main(rnd):
     hbm = statistics.median(pc_kib) * 1024.0 * factor
     traffic = {
         "workload": "batch512x10MiB", "kernel": "qsmd5_batch_pc64_kernel",
-        "source": "rocprofv3 --pmc FETCH_SIZE -- python3 bench.py --no-cpu-baseline --steps 2 "
-                  "--warmup 1 (own pass, no trace domains); raw: profiles/%s_pmc_fetch_size_bench.csv" % rnd,
+        "source": "rocprofv3 --pmc FETCH_SIZE -- python3 bench.py --no-cpu-baseline --no-config5 "
+                  "--steps 2 --warmup 1 (own pass, no trace domains); raw: profiles/%s_pmc_fetch_size_bench.csv" % rnd,
         "fetch_size_kib_raw_per_launch": statistics.median(pc_kib), "launches": len(pc_kib),
         "calibration": {"kernel": "k_stream_read (ubench/ubench_md5 calib): coalesced 16 B/lane "
                                   "dwordx4 read of 4 GiB",
