@@ -248,7 +248,27 @@ def config5_host_leg(args, rank, world, dev, cpu=False):
                          dist.get_backend() == "gloo" else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN)
         n = int(t.item())
-    shard = HostShard(n, rank, world, dev, cpu_rehearsal=cpu)
+    # The shard's pinned allocation can fail where the free-memory reading was
+    # optimistic (another tenant, a limit not visible here): then every rank
+    # skips the key together, and the headline line is still printed.
+    shard, err = None, ""
+    try:
+        shard = HostShard(n, rank, world, dev, cpu_rehearsal=cpu)
+    except Exception as e:  # qsmd5.Md5Error (-ENOMEM), torch OOM
+        err = "rank %d: %s" % (rank, e)
+        log("config5_host: %s" % err)
+    if dist_on:
+        ok_t = torch.tensor([0 if shard is None else 1], dtype=torch.int64,
+                            device="cpu" if cpu or dist.get_backend() == "gloo" else dev)
+        dist.all_reduce(ok_t, op=dist.ReduceOp.MIN)
+        all_ok = bool(ok_t.item())
+    else:
+        all_ok = shard is not None
+    if not all_ok:
+        if shard is not None:
+            shard.close()
+        return {"skipped": "a rank could not hold its shard of %d parts in pinned host memory%s"
+                           % (n, (": " + err) if err else "")}, True
     sync = (lambda: None) if cpu else torch.cuda.synchronize
     for _ in range(args.config5_warmup):
         shard.step()
