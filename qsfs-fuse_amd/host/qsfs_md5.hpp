@@ -189,6 +189,25 @@ inline std::string content_md5_from_hex(const std::string& hex) {
   return std::string(b, 24);
 }
 
+// The runtime's lifetime for a daemon's main() or FUSE init/destroy pair
+// (INTEGRATION.md §2): initialises the GPU runtime up front (after the fork
+// fuse_main does, Operations.cpp:1520-1549) and releases it with
+// qsmd5_shutdown() before static destructors run.  init() reports failure as
+// its return code; without a GPU the calls still hash on the CPU under the
+// default routing.  Stop every hashing thread and destroy every MD5 object
+// before the guard goes out of scope.
+class Runtime {
+ public:
+  Runtime() : init_rc_(qsmd5_init(0)) {}
+  Runtime(const Runtime&) = delete;
+  Runtime& operator=(const Runtime&) = delete;
+  ~Runtime() { (void)qsmd5_shutdown(); }
+  int init_rc() const { return init_rc_; }
+
+ private:
+  int init_rc_;
+};
+
 // class MD5 -- MD5.h:51-93, over the streaming C-ABI context.
 class MD5 {
  public:

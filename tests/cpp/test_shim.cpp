@@ -76,6 +76,14 @@ void expect(bool ok, const char* what) {
 }  // namespace
 
 int main() {
+  // The daemon's lifetime guard: init now, qsmd5_shutdown at the end of main.
+  qsmd5::Runtime runtime;
+  // 0. A shutdown in the middle re-initialises on the next call.
+  {
+    expect(md5(std::string("abc")) == "900150983cd24fb0d6963f7d28e17f72", "md5 before shutdown");
+    expect(qsmd5_shutdown() == 0 && qsmd5_shutdown() == 0, "qsmd5_shutdown twice");
+    expect(md5(std::string("abc")) == "900150983cd24fb0d6963f7d28e17f72", "md5 after shutdown");
+  }
   // 1. md5(std::string) -- global, as the reference's free function.
   std::printf("str_empty %s\n", md5(std::string()).c_str());
   std::printf("str_abc %s\n", md5(std::string("abc")).c_str());
