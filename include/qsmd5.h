@@ -202,9 +202,11 @@ QSMD5_API int qsmd5_free_pinned(void* ptr);
  * each batch's first touch, and rows in separate registered buffers are
  * gathered by one kernel per column.  The range is widened to
  * whole pages.  Unregister (with the same ptr) before freeing the memory.
- * -EINVAL for a NULL/empty range, a ptr registered twice, a range that
- * shares a page with one already registered, or unregistering a ptr this
- * library did not register. */
+ * -EINVAL for a NULL/empty range, a ptr registered twice, a range starting
+ * in the first page of one already registered, a range sharing a page with
+ * one already registered that HIP refuses, or unregistering a ptr this
+ * library did not register.  Ranges that share a boundary page (adjacent heap
+ * buffers) are otherwise fine: each is registered in full. */
 QSMD5_API int qsmd5_register_host(void* ptr, size_t bytes);
 QSMD5_API int qsmd5_unregister_host(void* ptr);
 

@@ -2106,14 +2106,22 @@ int qsmd5_register_host(void* ptr, size_t bytes) {
     const uintptr_t lo = u & ~(page - 1), hi = (u + bytes + page - 1) & ~(page - 1);
     Registry& R = registry();
     std::lock_guard<std::mutex> lk(R.mu);
-    if (R.base_of.count(u)) return fail(-EINVAL, "qsmd5: range already registered");
-    // Whole pages are registered, so two buffers that share a page cannot both
-    // be: refuse an overlap here instead of a generic hipHostRegister failure.
+    if (R.base_of.count(u) || R.end_of.count(lo))
+      return fail(-EINVAL, "qsmd5: range already registered, or starts in the first page of "
+                           "one (registration covers whole 4 KiB pages)");
+    // Heap buffers often share a boundary page with a neighbour (glibc hands
+    // out adjacent chunks once its mmap threshold has grown), and a pool
+    // registers them one by one.  HIP locks a page that is already locked
+    // again; if it refuses, say why instead of a generic -EIO.
     auto it = R.end_of.lower_bound(hi);
-    if (it != R.end_of.begin() && (--it)->second > lo)
-      return fail(-EINVAL, "qsmd5: range shares a page with a range already registered "
-                           "(registration covers whole 4 KiB pages)");
-    QS_HIP(hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault));
+    const bool overlaps = it != R.end_of.begin() && std::prev(it)->second > lo;
+    const hipError_t e = hipHostRegister(reinterpret_cast<void*>(lo), hi - lo, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+      if (!overlaps) return hip_fail(e, "hipHostRegister");
+      (void)hipGetLastError();
+      return fail(-EINVAL, std::string("qsmd5: range shares a page with a range already registered, "
+                                       "and HIP refused it: ") + hipGetErrorString(e));
+    }
     R.base_of[u] = lo;
     R.end_of[lo] = hi;
     return 0;

@@ -218,24 +218,35 @@ def test_gather_from_registered_pageable_buffers(pinned):
             qsmd5.unregister_host(b.ctypes.data)
 
 
-def test_register_refuses_a_shared_page():
-    """Registration covers whole 4 KiB pages: a second buffer in
-    a page already registered is refused with -EINVAL and a clear message,
-    not a generic hipHostRegister failure; after the first is unregistered it
-    can be registered."""
+def test_register_buffers_sharing_a_page():
+    """Registration covers whole 4 KiB pages.  Adjacent heap
+    buffers share a boundary page; a pool registers them one by one.  Either
+    both registrations succeed and both buffers hash correctly through the
+    gather path, or the second fails with -EINVAL naming the shared page --
+    never a generic -EIO.  A second range starting in the first page of a
+    registered one, or the same pointer twice, is -EINVAL."""
     import errno
-    blk = np.zeros(4 * 4096, dtype=np.uint8)
+    blk = np.zeros(6 * 4096, dtype=np.uint8)
+    blk[:] = np.random.default_rng(77).integers(0, 256, size=blk.size, dtype=np.uint8)
     base = (blk.ctypes.data + 4095) & ~4095
-    a, b = base + 100, base + 4096 + 2000  # a's range ends inside b's page
-    qsmd5.register_host(a, 4096 + 100)
+    a, la = base + 96, 2 * 4096 - 96 - 1000      # ends inside page 1
+    b, lb = a + la, 2 * 4096 + 1000 - 16          # starts in page 1, right after a
+    qsmd5.register_host(a, la)
     try:
         with pytest.raises(qsmd5.Md5Error) as e:
-            qsmd5.register_host(b, 512)
-        assert e.value.code == -errno.EINVAL and "shares a page" in str(e.value)
-        with pytest.raises(qsmd5.Md5Error) as e:
-            qsmd5.register_host(a, 16)  # the same pointer twice
+            qsmd5.register_host(base + 8, 16)     # starts in a's first page
         assert e.value.code == -errno.EINVAL
+        with pytest.raises(qsmd5.Md5Error) as e:
+            qsmd5.register_host(a, 16)            # the same pointer twice
+        assert e.value.code == -errno.EINVAL
+        try:
+            qsmd5.register_host(b, lb)
+            b_ok = True
+        except qsmd5.Md5Error as e2:
+            assert e2.code == -errno.EINVAL and "shares a page" in str(e2)
+            b_ok = False
+        _check([(a, la), (b, lb)] if b_ok else [(a, la)])
+        if b_ok:
+            qsmd5.unregister_host(b)
     finally:
         qsmd5.unregister_host(a)
-    qsmd5.register_host(b, 512)
-    qsmd5.unregister_host(b)
