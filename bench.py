@@ -202,14 +202,17 @@ def _host_mem_available():
                 avail = int(line.split()[1]) * 1024
     except (OSError, ValueError):
         pass
-    try:
-        cap = open("/sys/fs/cgroup/memory.max").read().strip()
-        if cap != "max":
-            used = int(open("/sys/fs/cgroup/memory.current").read().strip())
-            left = int(cap) - used
+    for cap_f, used_f in (("/sys/fs/cgroup/memory.max", "/sys/fs/cgroup/memory.current"),  # v2
+                          ("/sys/fs/cgroup/memory/memory.limit_in_bytes",            # v1
+                           "/sys/fs/cgroup/memory/memory.usage_in_bytes")):
+        try:
+            cap = open(cap_f).read().strip()
+            if cap == "max" or int(cap) >= 1 << 60:  # v1 writes ~2^63 for "no limit"
+                continue
+            left = int(cap) - int(open(used_f).read().strip())
             avail = left if avail is None else min(avail, left)
-    except (OSError, ValueError):
-        pass
+        except (OSError, ValueError):
+            pass
     return avail
 
 
