@@ -226,7 +226,12 @@ class MD5 {
   }
   ~MD5() { qsmd5_ctx_destroy(ctx_); }
 
+  // After finalize() the reference's update() folds the bytes into a state
+  // nobody reads again (finalize zeroised the count, MD5.cpp:306-309, and
+  // never runs twice): the digest and hexdigest() stay as they were.  The
+  // drop-in does the same -- a no-op -- rather than throw.
   void update(const unsigned char* buf, size_type length) {
+    if (finalized_) return;
     detail::check(qsmd5_ctx_update(ctx_, buf, length), "qsmd5_ctx_update");
   }
   void update(const char* buf, size_type length) {

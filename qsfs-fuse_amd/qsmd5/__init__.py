@@ -368,6 +368,10 @@ class MD5(object):
             self.finalize()
 
     def update(self, data):
+        # after finalize() the reference's update leaves the digest as it was
+        # (MD5.cpp:240-269, 284-312): a no-op here too
+        if self._digest is not None:
+            return self
         if isinstance(data, str):
             data = data.encode("latin-1")
         keep = []

@@ -130,6 +130,10 @@ int main() {
     std::printf("class_pieces %s\n", os.str().c_str());
     qsmd5::MD5 one(std::string("abc"));
     std::printf("class_ctor_abc %s\n", one.hexdigest().c_str());
+    // update after finalize: the reference keeps its digest (MD5.cpp:240-312)
+    one.update("more", 4);
+    one.finalize();
+    expect(one.hexdigest() == "900150983cd24fb0d6963f7d28e17f72", "update after finalize is a no-op");
   }
   // 5. Batch forms: md5_batch over ragged buffers, md5_file_parts over a
   //    25 MiB + 3 B "file" (PrepareUpload: 10, 10, 5 MiB + 3 B) and a 21 MiB one

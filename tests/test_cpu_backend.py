@@ -67,6 +67,9 @@ def test_stream_pieces_class(golden, monkeypatch):
             off += cut
         assert h.finalize().hexdigest() == case["md5"], case["cuts"][:4]
         assert h.hexdigest() == case["md5"]
+        # the reference's update() after finalize() leaves the digest as it was
+        h.update(b"more bytes")
+        assert h.finalize().hexdigest() == case["md5"]
 
 
 def test_ragged_and_sweep(golden):
