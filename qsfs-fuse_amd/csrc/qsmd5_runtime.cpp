@@ -188,10 +188,11 @@ pid_t g_init_pid = 0;                     // the process that owns the HIP state
 std::atomic<bool> g_forked_child{false};  // set in a child forked after init
 
 void on_fork_child() {
-  // HIP state does not survive fork(): a child of an initialised process
-  // must not touch the parent's streams or buffers (it hashes on the CPU
-  // under auto routing, see ensure_init).
-  if (g_init_state.load() != 0) g_forked_child.store(true);
+  // HIP state does not survive fork(): a child of a process in which this
+  // library ever initialised HIP (even if it shut its own runtime down since:
+  // HIP itself stays up) must not touch the GPU (it hashes on the CPU under
+  // auto routing, see ensure_init).  Registered at the first init.
+  if (g_init_pid != 0) g_forked_child.store(true);
 }
 
 // Devices to bind: QSMD5_DEVICES = "all" or a comma list of ordinals (an
@@ -1971,8 +1972,7 @@ int qsmd5_shutdown(void) {
     r.init_rc = 0;
     r.init_msg.clear();
     r.shard_bytes = 0;
-    g_forked_child.store(false);
-    g_init_state.store(0, std::memory_order_release);
+    g_init_state.store(0, std::memory_order_release);  // a forked child stays CPU-only
     if (rc) return fail(rc, "qsmd5_shutdown: a HIP release call failed (resources dropped anyway)");
     return 0;
   } catch (...) {
