@@ -41,8 +41,10 @@
  * Lazily initialised: the first call (or qsmd5_init) picks the current HIP
  * device, so it is safe to call after fuse_main() has forked (reference
  * Operations.cpp:1520-1549 initialises threads after the fork for the same
- * reason).  A child forked AFTER initialisation cannot use the parent's HIP
- * state: its GPU calls fail with -ENODEV, and auto routing hashes on the CPU.
+ * reason).  A child forked AFTER the library first initialised (even if
+ * qsmd5_shutdown ran since: HIP itself stays up in the parent) cannot use the
+ * parent's HIP state: its GPU calls fail with -ENODEV, and auto routing
+ * hashes on the CPU.
  *
  * Multi-GPU (one process, e.g. the qsfs daemon): QSMD5_DEVICES="all" or a
  * comma list of ordinals binds several GPUs at init.  qsmd5_hash_batch[_ex]
