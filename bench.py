@@ -469,16 +469,17 @@ def main():
         # VALU (bitop3, add3, alignbit, add).  Measured on gfx950 with one wave alone
         # on its SIMD (ubench chaincost, profiles/r02_chaincost.log): the steps from
         # registers take 1045 cycles per block; fed from the LDS ring (16
-        # ds_read_b128 per block) 1155.  The ceiling uses the register floor, at the
+        # ds_read_b128 per block, the shipped graded phase-start wait) 1133
+        # (profiles/r03_chaincost.log).  The ceiling uses the register floor, at the
         # 2.4 GHz the chip holds with a few CUs busy.
         "stream_ceiling": {
             "chains": ntot // world, "floor_cycles_per_block": 1045.0,
-            "lds_fed_floor_cycles_per_block": 1155.0,
+            "lds_fed_floor_cycles_per_block": 1133.0,
             "GBps": round(B * 64 * 2.4e9 / 1045.0 / 1e9, 2),
             "frac": round(achieved_gbs / (B * 64 * 2.4e9 / 1045.0 / 1e9), 4),
             "note": "achieved / (B x per-chain issue floor): how close the kernel is to what "
                     "B serial MD5 chains allow on one GPU; the floor has no operand "
-                    "traffic at all, so 1045 / 1155 = 0.905 is the most an LDS-fed chain "
+                    "traffic at all, so 1045 / 1133 = 0.922 is the most an LDS-fed chain "
                     "can reach"},
         "per_chain": {"GiBps": round(B * L / (1 << 30) / (kavg_ms * 1e-3) / B, 4),
                       "cycles_per_64B_block_at_2p4GHz": round(kavg_ms * 1e-3 * 2.4e9 / (L / 64), 1),

@@ -160,6 +160,218 @@ __global__ __launch_bounds__(128) void k_chain_cost(uint64_t* out, uint32_t* sin
   sink[lane] = st[0] ^ st[1] ^ st[2] ^ st[3];
 }
 
+// Round 3 (session 2): where could the chain's operands come from, if not the
+// LDS ring the producer shares with it?  The chain wave alone, continuous (no
+// phases, no barrier): block h+1's 16 operand groups are requested while block
+// h compresses, one wait per block.
+//   kSrc 0: LDS ring of 8 blocks (ds_read_b128)
+//   kSrc 1..3: a global ring of kRing blocks, buffer_load_dwordx4 with the
+//     cache policy aux = 0 (default), 1 (sc0: L2, the policy a ring written by
+//     another CU needs), 2 (nt)
+// out[0] = s_memtime cycles over `blocks` blocks.
+template <int kSrc, int kRing = 8>
+__global__ __launch_bounds__(128) void k_chain_ring(uint64_t* out, uint32_t* sink, int blocks,
+                                                    const u32x4* __restrict__ gring) {
+  __shared__ u32x4 ring[8][16][64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  if (kSrc == 0) {
+    for (int k = threadIdx.x; k < 8 * 16 * 64; k += blockDim.x)
+      (&ring[0][0][0])[k] = u32x4{(uint32_t)k * 2654435761u, (uint32_t)k, 7u, 9u};
+    __syncthreads();
+  }
+  if (wave == 1) return;
+  constexpr int kAux = kSrc == 1 ? 0 : kSrc == 2 ? 1 : 2;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)gring, 0, kRing * 16384, 0x00020000);
+  u32x4 a[16], b[16];
+  auto read_blk = [&](u32x4 (&dst)[16], uint32_t blk) {
+    const uint32_t slot = blk & (kRing - 1);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      if constexpr (kSrc == 0)
+        dst[g] = ring[blk & 7u][g][lane];
+      else
+        dst[g] = __builtin_bit_cast(
+            u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u + g * 1024u),
+                                                         (int)(slot * 16384u), kAux));
+    }
+  };
+  auto compress = [&](uint32_t (&st)[4], const u32x4 (&src)[16]) {
+    uint32_t mk[64];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      mk[4 * g + 0] = src[g].x;
+      mk[4 * g + 1] = src[g].y;
+      mk[4 * g + 2] = src[g].z;
+      mk[4 * g + 3] = src[g].w;
+    }
+    md5_compress_mk(st, mk);
+  };
+  constexpr int kWait = kSrc == 0 ? kLgkmcnt0 : 0x0F70;  // lgkmcnt(0) / vmcnt(0)
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  read_blk(a, 0);
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int h = 0; h < blocks; h += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kWait);
+    read_blk(b, h + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    compress(st, a);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kWait);
+    read_blk(a, h + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    compress(st, b);
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[0] = t1 - t0;
+  sink[lane] = st[0] ^ st[1] ^ st[2] ^ st[3];
+}
+
+// The same continuous chain over an L1-sized global ring of kSlots blocks with
+// kLanes live chains: slot = [16 groups][kLanes lanes] x 16 B, contiguous (the
+// L1 footprint; kCompact = false spreads the groups 1 KiB apart).  Dead
+// lanes keep EXEC full (a partial EXEC mask slows memory instructions) and
+// read past the buffer's range (num_records): zeros, no memory access.
+// kBar: an s_barrier after every block that a second wave meets (the
+// per-block hand-off a producer would need).
+template <int kSlots, int kLanes, bool kBar, bool kCompact = true>
+__global__ __launch_bounds__(128) void k_chain_l1(uint64_t* out, uint32_t* sink, int blocks,
+                                                  const u32x4* __restrict__ gring) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  if (wave == 1) {
+    if (kBar)
+      for (int p = 0; p < blocks + 1; ++p) __builtin_amdgcn_s_barrier();
+    return;
+  }
+  constexpr uint32_t kRow = kCompact ? kLanes * 16u : 1024u;  // bytes per group row
+  constexpr uint32_t kSlotB = 16u * kRow;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)gring, 0, kSlots * kSlotB, 0x00020000);
+  const uint32_t vbase = lane < (uint32_t)kLanes ? lane * 16u : 0x40000000u;
+  u32x4 a[16], b[16];
+  auto read_blk = [&](u32x4 (&dst)[16], uint32_t slot) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g)
+      dst[g] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(vbase + g * kRow),
+                                                       (int)(slot * kSlotB), 0));
+  };
+  auto compress = [&](uint32_t (&st)[4], const u32x4 (&src)[16]) {
+    uint32_t mk[64];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      mk[4 * g + 0] = src[g].x;
+      mk[4 * g + 1] = src[g].y;
+      mk[4 * g + 2] = src[g].z;
+      mk[4 * g + 3] = src[g].w;
+    }
+    md5_compress_mk(st, mk);
+  };
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  uint32_t slot = 0;
+  auto next = [&]() { slot = slot + 1 == (uint32_t)kSlots ? 0u : slot + 1; return slot; };
+  read_blk(a, 0);
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int h = 0; h < blocks; h += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    read_blk(b, next());
+    __builtin_amdgcn_sched_barrier(0);
+    compress(st, a);
+    if (kBar) __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    read_blk(a, next());
+    __builtin_amdgcn_sched_barrier(0);
+    compress(st, b);
+    if (kBar) __builtin_amdgcn_s_barrier();
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (kBar) __builtin_amdgcn_s_barrier();
+  if (lane == 0) out[0] = t1 - t0;
+  sink[lane] = st[0] ^ st[1] ^ st[2] ^ st[3];
+}
+
+// The hand-off the L1 ring would need: wave 1 stores block h+2 into slot
+// h % 2 while the chain compresses block h, drains its stores (vmcnt(0)) and
+// meets the chain at a per-block barrier; the chain waits for block h+1's
+// operands before that barrier, then requests block h+2's.  Does the chain
+// still hit L1 after another wave's stores, and does it see them?  Each group
+// g of block j holds {j, lane, g, 0x5a}; out[1] counts the chain's mismatches.
+// kStoreAux: the producer's store cache policy.
+template <int kStoreAux>
+__global__ __launch_bounds__(128) void k_l1_handoff(uint64_t* out, uint32_t* sink, int blocks,
+                                                    u32x4* __restrict__ gring) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const auto rs = __builtin_amdgcn_make_buffer_rsrc((void*)gring, 0, 2 * 16384, 0x00020000);
+  if (wave == 1) {
+    auto put = [&](uint32_t blk) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(__attribute__((ext_vector_type(4))) int,
+                               u32x4{blk, lane, (uint32_t)g, 0x5au}),
+            rs, (int)(lane * 16u + g * 1024u), (int)((blk & 1u) * 16384u), kStoreAux);
+    };
+    put(0);
+    put(1);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_barrier();
+    for (int h = 0; h < blocks; ++h) {
+      put((uint32_t)h + 2u);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      __builtin_amdgcn_s_barrier();
+    }
+    return;
+  }
+  u32x4 a[16], b[16];
+  auto read_blk = [&](u32x4 (&dst)[16], uint32_t blk) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g)
+      dst[g] = __builtin_bit_cast(
+          u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 16u + g * 1024u),
+                                                       (int)((blk & 1u) * 16384u), 0));
+  };
+  uint32_t bad = 0;
+  auto compress = [&](uint32_t (&st)[4], const u32x4 (&src)[16], uint32_t blk) {
+    uint32_t mk[64];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      bad += (src[g].x != blk) | (src[g].y != lane) | (src[g].z != (uint32_t)g);
+      mk[4 * g + 0] = src[g].x;
+      mk[4 * g + 1] = src[g].y;
+      mk[4 * g + 2] = src[g].z;
+      mk[4 * g + 3] = src[g].w;
+    }
+    md5_compress_mk(st, mk);
+  };
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  __builtin_amdgcn_s_barrier();
+  read_blk(a, 0);
+  __builtin_amdgcn_s_waitcnt(0x0F70);
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int h = 0; h < blocks; h += 2) {
+    __builtin_amdgcn_sched_barrier(0);
+    read_blk(b, (uint32_t)h + 1u);
+    __builtin_amdgcn_sched_barrier(0);
+    compress(st, a, (uint32_t)h);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    read_blk(a, (uint32_t)h + 2u);
+    __builtin_amdgcn_sched_barrier(0);
+    compress(st, b, (uint32_t)h + 1u);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_barrier();
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[0] = t1 - t0;
+  bad = __builtin_amdgcn_readfirstlane(bad) + 0u;  // lane 0's count is enough for a probe
+  if (lane == 0) out[1] = bad;
+  sink[lane] = st[0] ^ st[1] ^ st[2] ^ st[3];
+}
+
 // Latency kernel with 5-block phases: a 160 KiB ring (all of a gfx950 CU's
 // LDS), one barrier per 5 blocks instead of per 4.
 // producer sleeps kP x ~64 cycles after each phase barrier before writing the
@@ -1245,6 +1457,59 @@ int main(int argc, char** argv) {
     one(k_chain_cost<0, 64, 16>, "chain_phase, graded wait on block 0 (lead 16 steps)");
     one(k_chain_cost<0, 64, 32>, "chain_phase, graded wait on block 0 (lead 32 steps)");
     one(k_chain_cost<1, 64, 16>, "+ lds_barrier per 4 blocks, lead 16");
+    // operands from a continuous ring, no phases (k_chain_ring)
+    u32x4* d_ring;
+    CK(hipMalloc(&d_ring, 64 * 16384));
+    {
+      std::vector<uint32_t> h(64 * 4096);
+      for (size_t i = 0; i < h.size(); ++i) h[i] = (uint32_t)i * 2654435761u;
+      CK(hipMemcpy(d_ring, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    }
+    const int nb = phases * kPcHalf;
+    auto ring_one = [&](auto kern, const char* what) {
+      hipLaunchKernelGGL(kern, dim3(1), dim3(128), 0, 0, d_out, d_sink, 64, d_ring);
+      hipLaunchKernelGGL(kern, dim3(1), dim3(128), 0, 0, d_out, d_sink, nb, d_ring);
+      CK(hipDeviceSynchronize());
+      uint64_t cyc;
+      CK(hipMemcpy(&cyc, d_out, 8, hipMemcpyDeviceToHost));
+      printf("  %-58s %.1f cycles/block\n", what, (double)cyc / nb);
+    };
+    ring_one(k_chain_ring<0>, "continuous LDS ring (no phases, no barrier)");
+    ring_one(k_chain_ring<1, 2>, "global ring 2 blocks, default policy");
+    ring_one(k_chain_ring<1, 8>, "global ring 8 blocks, default policy");
+    ring_one(k_chain_ring<2, 8>, "global ring 8 blocks, sc0 (L2)");
+    ring_one(k_chain_ring<2, 64>, "global ring 64 blocks, sc0 (L2)");
+    ring_one(k_chain_ring<3, 64>, "global ring 64 blocks, nt");
+    ring_one(k_chain_l1<2, 64, false>, "L1 ring 2 slots x 64 lanes (32 KiB)");
+    ring_one(k_chain_l1<2, 64, true>, "L1 ring 2 slots x 64 lanes, barrier per block");
+    ring_one(k_chain_l1<3, 32, false, false>, "L1 ring 3 slots x 32 live lanes, 1 KiB rows");
+    ring_one(k_chain_l1<3, 32, false>, "L1 ring 3 slots x 32 live lanes (24 KiB)");
+    ring_one(k_chain_l1<3, 32, true>, "L1 ring 3 slots x 32 live lanes, barrier per block");
+    ring_one(k_chain_l1<4, 32, true>, "L1 ring 4 slots x 32 live lanes (32 KiB), barrier");
+    ring_one(k_chain_l1<2, 32, true>, "L1 ring 2 slots x 32 live lanes (16 KiB), barrier");
+    ring_one(k_chain_l1<5, 16, true>, "L1 ring 5 slots x 16 live lanes (20 KiB), barrier");
+    ring_one(k_chain_l1<8, 16, true>, "L1 ring 8 slots x 16 live lanes (32 KiB), barrier");
+    ring_one(k_chain_l1<4, 16, true>, "L1 ring 4 slots x 16 live lanes (16 KiB), barrier");
+    ring_one(k_chain_l1<2, 16, true>, "L1 ring 2 slots x 16 live lanes (8 KiB), barrier");
+    ring_one(k_chain_l1<1, 64, false>, "L1 ring 1 slot x 64 lanes (16 KiB)");
+    {
+      uint64_t* d_o2;
+      CK(hipMalloc(&d_o2, 16));
+      auto hand = [&](auto kern, const char* what) {
+        hipLaunchKernelGGL(kern, dim3(1), dim3(128), 0, 0, d_o2, d_sink, 64, d_ring);
+        hipLaunchKernelGGL(kern, dim3(1), dim3(128), 0, 0, d_o2, d_sink, nb, d_ring);
+        CK(hipDeviceSynchronize());
+        uint64_t r[2];
+        CK(hipMemcpy(r, d_o2, 16, hipMemcpyDeviceToHost));
+        printf("  %-58s %.1f cycles/block, %llu stale operand groups\n", what, (double)r[0] / nb,
+               (unsigned long long)r[1]);
+      };
+      hand(k_l1_handoff<0>, "hand-off: 2 slots, producer stores, default policy");
+      hand(k_l1_handoff<1>, "hand-off: 2 slots, producer stores sc0");
+      hand(k_l1_handoff<2>, "hand-off: 2 slots, producer stores nt");
+      CK(hipFree(d_o2));
+    }
+    CK(hipFree(d_ring));
     CK(hipFree(d_out));
     CK(hipFree(d_sink));
     return 0;
