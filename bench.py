@@ -245,7 +245,7 @@ def config5_host_leg(args, rank, world, dev, cpu=False):
         local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
         nodes = max(1, world // max(1, local_world))
         fit = int(avail * 0.6) // PART * nodes
-        n = max(world, min(want, fit))
+        n = min(want, max(world, fit))  # cut to fit, but never below a part per rank
     if dist_on:
         t = torch.tensor([n], dtype=torch.int64, device="cpu" if cpu or
                          dist.get_backend() == "gloo" else dev)
