@@ -184,6 +184,26 @@ def test_bench_two_rank_rehearsal():
     assert c5["parts_per_rank"] == [20, 20] and c5["parity"] == "ok: 40/40 digests == reference golden"
 
 
+def test_bench_rehearsal_rank_without_parts():
+    """Three ranks share the card over gloo and the config5_host object has
+    only two parts: rank 0 holds none (an empty pinned shard, no launch, an
+    empty digest block in the gather), and every digest still arrives."""
+    cmd = [PY, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "3", "--steps", "1", "--warmup", "1",
+           "--batch", "16", "--rehearse-gloo", "--config5-parts", "2", "--config5-reps", "1",
+           "--config5-warmup", "0"]
+    out = subprocess.run(cmd, env=ENV, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 3 and r["parity"].startswith("ok: 48/48")
+    c5 = r["config5_host"]
+    assert c5["parts"] == 2 and c5["parts_per_rank"] == [0, 1, 1]
+    assert c5["parity"] == "ok: 2/2 digests == reference golden"
+
+
 def test_bench_rccl_path_world_one():
     """The RCCL path of bench.py (nccl process group bound to the device,
     all_gather_into_tensor of the digests, all_reduce MAX of the time) run at
