@@ -227,6 +227,60 @@ __global__ __launch_bounds__(128) void k_chain_ring(uint64_t* out, uint32_t* sin
   sink[lane] = st[0] ^ st[1] ^ st[2] ^ st[3];
 }
 
+// The continuous LDS chain with block h+1's 16 operand reads issued after
+// step kS of block h instead of at its start (the graded phase-start wait puts
+// block 1's reads after step 8 of block 0; is that placement better for every
+// block?).  kS = 0 is k_chain_ring<0>.
+template <int kS>
+__global__ __launch_bounds__(128) void k_chain_at(uint64_t* out, uint32_t* sink, int blocks,
+                                                  const u32x4* __restrict__ gring) {
+  (void)gring;
+  __shared__ u32x4 ring[8][16][64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  for (int k = threadIdx.x; k < 8 * 16 * 64; k += blockDim.x)
+    (&ring[0][0][0])[k] = u32x4{(uint32_t)k * 2654435761u, (uint32_t)k, 7u, 9u};
+  __syncthreads();
+  if (wave == 1) return;
+  u32x4 a[16], b[16];
+  auto read_blk = [&](u32x4 (&dst)[16], uint32_t blk) {
+#pragma unroll
+    for (int g = 0; g < 16; ++g) dst[g] = ring[blk & 7u][g][lane];
+  };
+  uint32_t st[4] = {kInit0, kInit1, kInit2, kInit3};
+  auto block = [&](const u32x4 (&cur)[16], u32x4 (&nxt)[16], uint32_t next_blk) {
+    uint32_t mk[64];
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      mk[4 * g + 0] = cur[g].x;
+      mk[4 * g + 1] = cur[g].y;
+      mk[4 * g + 2] = cur[g].z;
+      mk[4 * g + 3] = cur[g].w;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_waitcnt(kLgkmcnt0);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t v[4] = {st[0], st[1], st[2], st[3]};
+    if constexpr (kS > 0) md5_steps_mk<0, kS>(v, mk);
+    __builtin_amdgcn_sched_barrier(0);
+    read_blk(nxt, next_blk);
+    __builtin_amdgcn_sched_barrier(0);
+    md5_steps_mk<kS, 64>(v, mk);
+    st[0] += v[0];
+    st[1] += v[1];
+    st[2] += v[2];
+    st[3] += v[3];
+  };
+  read_blk(a, 0);
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  for (int h = 0; h < blocks; h += 2) {
+    block(a, b, h + 1);
+    block(b, a, h + 2);
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) out[0] = t1 - t0;
+  sink[lane] = st[0] ^ st[1] ^ st[2] ^ st[3];
+}
+
 // The same continuous chain over an L1-sized global ring of kSlots blocks with
 // kLanes live chains: slot = [16 groups][kLanes lanes] x 16 B, contiguous (the
 // L1 footprint; kCompact = false spreads the groups 1 KiB apart).  Dead
@@ -1475,6 +1529,11 @@ int main(int argc, char** argv) {
       printf("  %-58s %.1f cycles/block\n", what, (double)cyc / nb);
     };
     ring_one(k_chain_ring<0>, "continuous LDS ring (no phases, no barrier)");
+    ring_one(k_chain_at<0>, "continuous LDS, next reads after step 0");
+    ring_one(k_chain_at<4>, "continuous LDS, next reads after step 4");
+    ring_one(k_chain_at<8>, "continuous LDS, next reads after step 8");
+    ring_one(k_chain_at<16>, "continuous LDS, next reads after step 16");
+    ring_one(k_chain_at<32>, "continuous LDS, next reads after step 32");
     ring_one(k_chain_ring<1, 2>, "global ring 2 blocks, default policy");
     ring_one(k_chain_ring<1, 8>, "global ring 8 blocks, default policy");
     ring_one(k_chain_ring<2, 8>, "global ring 8 blocks, sc0 (L2)");
