@@ -33,7 +33,8 @@
  *     digest (never an empty Content-MD5).  A sticky HIP error
  *     (a lost GPU context) is logged once to stderr and every later call of
  *     the process hashes on the CPU; qsmd5_get_stats reports it.
- *     QSMD5_LOG=1 logs each call's backend, reason and size to stderr.
+ *     qsmd5_set_log_callback sends each call's backend, reason and size to
+ *     the host's logger (QSMD5_LOG=1: to stderr).
  *   - lengths up to 2^38 bytes per chunk; the full 64-bit MD5 length is used.
  *     The reference truncates lengths >= 4 GiB (MD5.h:53 32-bit size_type,
  *     MD5.cpp:106); set QSMD5_FLAG_REF_TRUNCATE32 to reproduce that.
@@ -112,15 +113,41 @@ QSMD5_API int qsmd5_init(int flags);
  * descriptor/digest scratch, staging ring and pinned metadata, and every host
  * range still registered through qsmd5_register_host -- before static
  * destructors run (a qsfs daemon's exit path; the reference has no such step:
- * MD5 holds no global state, MD5.cpp:283).  Waits for a batch in flight on a
- * GPU to finish.  No other call may start during it, and streaming contexts
- * must be destroyed first.  Idempotent: 0 when there is nothing to release.
- * A later call initialises afresh.  In a child forked after initialisation it
- * drops the parent's handles without a HIP call.  Returns 0, or -EIO if a
- * HIP release call failed (the resources are dropped either way). */
+ * MD5 holds no global state, MD5.cpp:283).  Waits until every call in flight
+ * on any thread has returned; calls that start meanwhile wait for it and then
+ * initialise afresh.  Streaming contexts must be destroyed first.  Called from
+ * inside a qsmd5 call on the same thread it returns -EINVAL.  Idempotent: 0
+ * when there is nothing to release.  In a child forked after initialisation it
+ * drops the parent's handles without a HIP call and without a lock.  Returns
+ * 0, or -EIO if a HIP release call failed (the resources are dropped either
+ * way). */
 QSMD5_API int qsmd5_shutdown(void);
 
 QSMD5_API int qsmd5_abi_version(void);
+
+/* Log sink for the library's messages (the digest backend and
+ * batch size at qsfs's DebugInfo).  Levels are qsfs's LogLevel::Value
+ * (src/base/LogLevel.h:27).  Once a sink is set, every message goes to it and
+ * nothing to stderr:
+ *   QSMD5_LOG_INFO   each hashing call's backend, reason, chunk count and
+ *                    bytes ("qsmd5: backend=gpu reason=size chunks=64
+ *                    bytes=671088640"), and the GPUs bound at initialisation;
+ *   QSMD5_LOG_WARN   a GPU batch that failed and was re-hashed on the CPU, a
+ *                    GPU runtime that could not initialise;
+ *   QSMD5_LOG_ERROR  a lost GPU context (all later calls hash on the CPU).
+ * `msg` has no trailing newline and is valid only during the call.  The sink
+ * runs on the thread that made the qsmd5 call, possibly several at once; it
+ * must not call back into this library.  NULL restores the default: warnings
+ * and errors to stderr, Info lines only under QSMD5_LOG=1.  A qsfs binding:
+ *   static void qsfs_md5_log(int lvl, const char* m, void*) {
+ *     if (lvl == QSMD5_LOG_INFO) DebugInfo(m); else if (lvl == QSMD5_LOG_WARN)
+ *     DebugWarning(m); else DebugError(m); }
+ *   qsmd5_set_log_callback(qsfs_md5_log, NULL);   // in qsfs_init */
+#define QSMD5_LOG_INFO 0
+#define QSMD5_LOG_WARN 1
+#define QSMD5_LOG_ERROR 2
+typedef void (*qsmd5_log_fn)(int level, const char* msg, void* user);
+QSMD5_API int qsmd5_set_log_callback(qsmd5_log_fn fn, void* user);
 
 /* Number of HIP devices visible to this process (0 without a GPU); does not
  * initialise the runtime. */
@@ -268,8 +295,9 @@ QSMD5_API int qsmd5_route(const qsmd5_chunk* chunks, size_t n, int flags);
 
 /* The rates QSMD5_BACKEND=auto prices a batch with (qsmd5_route), in GiB/s.
  * They are this host's: the CPU rates are timed once, at the first routing
- * decision (~1 ms); the GPU chain rate comes from the latest single-launch
- * GPU batch of <= 16 384 chunks whose longest is >= 4 MiB (0.119 before any).
+ * decision (~1 ms); the GPU chain rate is averaged over single-launch GPU
+ * batches of <= 16 384 chunks whose longest is >= 4 MiB, each bound GPU's
+ * first such batch not counted (0.119 before any; reset by qsmd5_shutdown).
  * QSMD5_CPU_GIBS, QSMD5_GPU_CHAIN_GIBS and QSMD5_LINK_GIBS override;
  * QSMD5_CALIBRATE=0 keeps the built-in CPU defaults. */
 #define QSMD5_RATE_CPU_MEASURED 1   /* cpu_chain_gibs / cpu_lane_thread_gibs timed on this host */
@@ -295,7 +323,9 @@ typedef struct qsmd5_stats {
   uint64_t fallbacks;    /* of those, calls whose GPU attempt failed */
   uint64_t gpu_chunks, cpu_chunks;
   int gpu_lost;          /* 1 once a sticky HIP error was seen: all later calls run on the CPU */
-  int reserved;
+  int inits;             /* runtime initialisations (HIP device setup) this process ran: 1 after
+                          * the first call, +1 per re-init after qsmd5_shutdown; a forked child
+                          * never adds one (it makes no HIP call) */
 } qsmd5_stats;
 QSMD5_API int qsmd5_get_stats(qsmd5_stats* out);
 

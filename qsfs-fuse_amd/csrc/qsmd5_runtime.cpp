@@ -21,6 +21,7 @@
 #include <errno.h>
 #include <hip/hip_runtime.h>
 #include <pthread.h>
+#include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -35,6 +36,7 @@
 #include <memory>
 #include <new>
 #include <numeric>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -64,6 +66,39 @@ thread_local std::string t_last_error;
 int fail(int code, const std::string& what) {
   t_last_error = what;
   return code;
+}
+
+// ---- log sink -----------------------------------------------------------------
+// qsfs logs through glog macros (base/LogMacros.h) and
+// should see the digest backend and batch size at DebugInfo, next to its
+// upload lines (QSClient.cpp:378-380).  A FUSE daemon's stderr is usually
+// gone, so qsmd5_set_log_callback hands every line to the host's logger
+// instead; levels are qsfs's LogLevel::Value (base/LogLevel.h:27).  Without a
+// sink, warnings and errors go to stderr, and Info lines only under QSMD5_LOG=1.
+struct LogSink {
+  qsmd5_log_fn fn;
+  void* user;
+};
+std::atomic<const LogSink*> g_log_sink{nullptr};  // replaced sinks are leaked: a logger
+                                                  // thread may still be reading one
+
+bool log_wanted(int level) {
+  static const bool env_on = getenv("QSMD5_LOG") && strcmp(getenv("QSMD5_LOG"), "0") != 0;
+  return g_log_sink.load(std::memory_order_acquire) != nullptr || level >= QSMD5_LOG_WARN || env_on;
+}
+
+__attribute__((format(printf, 2, 3))) void log_msg(int level, const char* fmt, ...) {
+  if (!log_wanted(level)) return;
+  char line[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(line, sizeof(line), fmt, ap);
+  va_end(ap);
+  if (const LogSink* s = g_log_sink.load(std::memory_order_acquire)) {
+    s->fn(level, line, s->user);
+    return;
+  }
+  fprintf(stderr, "%s\n", line);
 }
 
 int hip_fail(hipError_t e, const char* what) {
@@ -160,6 +195,7 @@ struct Dev {
   hipEvent_t ev_meta = nullptr, ev_first = nullptr, ev_last = nullptr;
   uint64_t staging_cap = kDefaultStaging;
   double last_wall_ms = 0, last_kernel_ms = 0;
+  std::atomic<uint32_t> chain_samples{0};  // batches that qualified as a chain-rate sample
 };
 
 struct Runtime {
@@ -297,7 +333,10 @@ int release_dev(Dev& d) {
   return bad;
 }
 
+std::atomic<int> g_inits{0};  // do_init runs (qsmd5_stats.inits)
+
 void do_init() {
+  g_inits.fetch_add(1);
   Runtime& r = rt();
   int n = 0;
   hipError_t e = hipGetDeviceCount(&n);
@@ -325,9 +364,24 @@ void do_init() {
   (void)hipSetDevice(r.devs[0]->device);
   r.ready = true;
   r.init_rc = 0;
+  if (log_wanted(QSMD5_LOG_INFO))
+    for (const Dev* d : r.devs) {
+      hipDeviceProp_t p;
+      if (hipGetDeviceProperties(&p, d->device) != hipSuccess) {
+        (void)hipGetLastError();
+        continue;
+      }
+      log_msg(QSMD5_LOG_INFO, "qsmd5: bound GPU %d (%s, %d CUs), staging ring up to %llu MiB", d->device,
+           p.gcnArchName, p.multiProcessorCount, (unsigned long long)(d->staging_cap >> 20));
+    }
 }
 
 int ensure_init() {
+  // A forked child first: no HIP call at all, not even a (re-)initialisation
+  // after the parent or the child itself shut the runtime down.
+  if (g_forked_child.load(std::memory_order_relaxed))
+    return fail(-ENODEV, "qsmd5: the GPU runtime was initialised before fork(); a forked child "
+                         "cannot use it (initialise after the fork, as qsfs does)");
   if (g_init_state.load(std::memory_order_acquire) == 0) {
     std::lock_guard<std::mutex> lk(g_init_mu);
     if (g_init_state.load() == 0) {
@@ -336,11 +390,13 @@ int ensure_init() {
       g_init_pid = getpid();
       do_init();
       g_init_state.store(rt().ready ? 1 : 2, std::memory_order_release);
+      if (!rt().ready)
+        log_msg(QSMD5_LOG_WARN, "qsmd5: GPU runtime not available (%s); %s", rt().init_msg.c_str(),
+             getenv("QSMD5_BACKEND") && !strcmp(getenv("QSMD5_BACKEND"), "gpu")
+                 ? "QSMD5_BACKEND=gpu: hashing calls fail"
+                 : "hashing on the CPU");
     }
   }
-  if (g_forked_child.load(std::memory_order_relaxed))
-    return fail(-ENODEV, "qsmd5: the GPU runtime was initialised before fork(); a forked child "
-                         "cannot use it (initialise after the fork, as qsfs does)");
   Runtime& r = rt();
   if (!r.ready) return fail(r.init_rc ? r.init_rc : -ENODEV, r.init_msg);
   // Calls may come from threads whose current device differs.
@@ -617,20 +673,34 @@ uint32_t pc_lanes_for(size_t n, uint64_t longest) {
 using qsmd5::kNoColumns;
 using qsmd5::stage_bytes;
 
-// The GPU chain rate of the latest timed batch (double bits; 0 = none yet),
+// The GPU chain rate averaged over timed batches (double bits; 0 = none yet),
 // for the routing cost model ("backend routing" below).  Only a batch that ran
 // as ONE latency-kernel launch (<= 16 384 chunks, one chain per lane) with a
 // longest chunk of >= 4 MiB measures a chain: its kernel time is that chain's.
 std::atomic<uint64_t> g_gpu_chain_bits{0};
 
-void note_gpu_chain(uint64_t longest, size_t n, unsigned launches, double kernel_ms) {
+// One outlier must not steer routing: the first qualifying batch
+// of each bound GPU is not used (deferred code-object loading and clock
+// ramp-up can fall inside its window), a sample outside [0.03, 0.6] GiB/s --
+// the ~1190 cycles per 64-B block expected at 2.4 GHz is 0.12 -- is not a
+// chain-bound launch, and the rest are folded into an average (new samples
+// weigh 1/4), so one slow launch on a shared GPU moves it by a quarter at most.
+void note_gpu_chain(std::atomic<uint32_t>& dev_samples, uint64_t longest, size_t n, unsigned launches,
+                    double kernel_ms) {
   if (launches != 1 || n > qsmd5::kLatencyKernelResident || longest < (4ull << 20) || kernel_ms <= 0)
     return;
+  if (dev_samples.fetch_add(1, std::memory_order_relaxed) == 0) return;  // this GPU's first
   const double gibs = (double)longest / (kernel_ms * 1e-3) / 1073741824.0;
-  if (gibs < 0.01 || gibs > 10.0) return;  // not a chain-bound launch
-  uint64_t bits;
-  memcpy(&bits, &gibs, sizeof(bits));
-  g_gpu_chain_bits.store(bits, std::memory_order_relaxed);
+  if (gibs < 0.03 || gibs > 0.6) return;
+  uint64_t old = g_gpu_chain_bits.load(std::memory_order_relaxed), bits;
+  do {
+    double avg = gibs;
+    if (old) {
+      memcpy(&avg, &old, sizeof(avg));
+      avg = 0.75 * avg + 0.25 * gibs;
+    }
+    memcpy(&bits, &avg, sizeof(bits));
+  } while (!g_gpu_chain_bits.compare_exchange_weak(old, bits, std::memory_order_relaxed));
 }
 
 // The synchronous batch on one GPU: device chunks in one launch; host chunks
@@ -1021,7 +1091,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   {
     uint64_t longest = 0;
     for (uint64_t L : len) longest = std::max(longest, L);
-    note_gpu_chain(longest, n, launches, r.last_kernel_ms);
+    note_gpu_chain(r.chain_samples, longest, n, launches, r.last_kernel_ms);
   }
   r.last_wall_ms =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -1317,8 +1387,37 @@ struct DeviceRestore {
   }
 };
 
+// Calls in flight against qsmd5_shutdown: every entry point
+// that may reach the runtime holds g_calls shared for its whole duration (the
+// outermost one on a thread; entry points call each other), and shutdown takes
+// it exclusively, so it waits for every call in flight -- the group-commit
+// leader's merged batch, a split batch's CPU thread, a sharded batch's threads
+// all run inside some caller's call -- and calls that arrive meanwhile wait
+// for it, then initialise afresh.  A child forked after init takes no lock: a
+// parent thread may have held it at fork(), and the child never touches the
+// parent's HIP state anyway.
+std::shared_mutex g_calls;
+thread_local int t_call_depth = 0;
+
+struct CallScope {
+  bool locked = false;
+  CallScope() {
+    if (t_call_depth++ == 0 && !g_forked_child.load(std::memory_order_relaxed)) {
+      g_calls.lock_shared();
+      locked = true;
+    }
+  }
+  ~CallScope() {
+    --t_call_depth;
+    if (locked) g_calls.unlock_shared();
+  }
+  CallScope(const CallScope&) = delete;
+  CallScope& operator=(const CallScope&) = delete;
+};
+
 template <class F>
 int guarded(F&& f) {
+  CallScope call;
   DeviceRestore keep;
   try {
     return f();
@@ -1350,9 +1449,10 @@ int guarded(F&& f) {
 // The rates are this host's, not constants: r_cpu is
 // timed once, at the first routing decision, on a 128 KiB buffer (~0.2 ms;
 // best of 3), and so is one thread's 16-lane AVX-512 group when the host has
-// it; r_gpu is taken from the kernel time of the latest single-launch GPU
-// batch of <= 16 384 chunks whose longest chunk is >= 4 MiB (one chain per
-// lane: the regime the estimate describes), and is 0.119 GiB/s until then.
+// it; r_gpu is averaged over the kernel times of single-launch GPU batches
+// of <= 16 384 chunks whose longest chunk is >= 4 MiB (one chain per lane:
+// the regime the estimate describes; each GPU's first such batch is skipped,
+// note_gpu_chain), and is 0.119 GiB/s until then.
 // QSMD5_CPU_GIBS / QSMD5_GPU_CHAIN_GIBS / QSMD5_LINK_GIBS override them;
 // QSMD5_CALIBRATE=0 keeps the defaults.  qsmd5_get_rates reports what is used.
 constexpr double kGpuChainGiBs = 0.119;  // until a batch has been timed on this GPU
@@ -1743,12 +1843,11 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
 }
 
 void log_call(const char* backend, const char* reason, size_t n, const qsmd5_chunk* chunks) {
-  static const bool on = env_u64("QSMD5_LOG", 0) != 0;
-  if (!on) return;
+  if (!log_wanted(QSMD5_LOG_INFO)) return;
   uint64_t total = 0;
   for (size_t i = 0; i < n; ++i) total += chunks[i].len;
-  fprintf(stderr, "qsmd5: backend=%s reason=%s chunks=%zu bytes=%llu\n", backend, reason, n,
-          (unsigned long long)total);
+  log_msg(QSMD5_LOG_INFO, "qsmd5: backend=%s reason=%s chunks=%zu bytes=%llu", backend, reason, n,
+       (unsigned long long)total);
 }
 
 // After a failed GPU batch: is the HIP context gone for good (a sticky error
@@ -1766,8 +1865,8 @@ void note_gpu_failure(int rc, bool injected_sticky) {
     }
   }
   if (lost && !g_gpu_lost.exchange(true))
-    fprintf(stderr, "qsmd5: GPU context lost (%s); hashing on the CPU from now on -- restart the "
-            "process to use the GPU again\n", why.c_str());
+    log_msg(QSMD5_LOG_ERROR, "qsmd5: GPU context lost (%s); hashing on the CPU from now on -- restart "
+         "the process to use the GPU again", why.c_str());
 }
 
 // One GPU attempt, with the test-only fault injection (QSMD5_INJECT_GPU_FAULT:
@@ -1838,6 +1937,9 @@ int run_split(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int g
     if (rc == -EINVAL) return rc;
     note_gpu_failure(rc, sticky);
     const std::string gpu_err = t_last_error;
+    if (rc != -ENODEV)
+      log_msg(QSMD5_LOG_WARN, "qsmd5: GPU share (%zu chunks) of a split batch failed (%s); "
+              "re-hashing it on the CPU", gc.size(), gpu_err.c_str());
     if (int rc2 = cpu_batch(gc.data(), gc.size(), gdig, gflags))
       return fail(rc2, t_last_error + " (after GPU failure: " + gpu_err + ")");
     g_fallbacks.fetch_add(1);
@@ -1893,6 +1995,9 @@ int hash_routed(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
   if (b == kGpu || rc == -EINVAL) return rc;
   note_gpu_failure(rc, sticky);
   const std::string gpu_err = t_last_error;
+  if (rc != -ENODEV)  // no usable GPU at all was logged once, at the failed initialisation
+    log_msg(QSMD5_LOG_WARN, "qsmd5: GPU batch of %zu chunks failed (%s); re-hashing it on the CPU",
+            n, gpu_err.c_str());
   const int rc2 = on_cpu("fallback");
   if (rc2) return fail(rc2, t_last_error + " (after GPU failure: " + gpu_err + ")");
   g_fallbacks.fetch_add(1);
@@ -1935,25 +2040,32 @@ int qsmd5_init(int flags) {
 }
 
 int qsmd5_shutdown(void) {
+  // In a child forked after init the HIP handles are the parent's: drop them
+  // without a HIP call and without taking a lock another parent thread may
+  // have held at fork() (the Dev objects and their memory are leaked; they go
+  // with the child's exit).  Later calls in the child hash on the CPU.
+  if (g_forked_child.load()) {
+    g_init_state.store(0, std::memory_order_release);
+    return 0;
+  }
+  if (t_call_depth > 0)
+    return fail(-EINVAL, "qsmd5_shutdown: called from inside a qsmd5 call on this thread");
   try {
+    std::unique_lock<std::shared_mutex> calls(g_calls);  // every call in flight has returned
     std::lock_guard<std::mutex> lk(g_init_mu);
     Runtime& r = rt();
-    // In a child forked after init the HIP handles are the parent's: drop
-    // them without a HIP call (the memory goes with the child's exit).
-    const bool own_hip = g_init_pid == getpid() && !g_forked_child.load();
+    const bool own_hip = g_init_pid == getpid();
     int prev = -1;
     if (own_hip && !r.devs.empty() && hipGetDevice(&prev) != hipSuccess) {
       prev = -1;
       (void)hipGetLastError();
     }
     int rc = 0;
-    for (Dev* d : r.devs) {
-      {
-        std::lock_guard<std::mutex> dl(d->mu);  // a batch still in flight finishes first
-        if (own_hip && release_dev(*d) != 0 && rc == 0) rc = -EIO;
-      }
+    for (Dev* d : r.devs) {  // no call is in flight: nothing else can hold d->mu
+      if (own_hip && release_dev(*d) != 0 && rc == 0) rc = -EIO;
       delete d;
     }
+    g_gpu_chain_bits.store(0, std::memory_order_relaxed);  // a re-init times its GPU afresh
     r.devs.clear();
     {
       Registry& R = registry();
@@ -1981,6 +2093,16 @@ int qsmd5_shutdown(void) {
 }
 
 int qsmd5_abi_version(void) { return QSMD5_ABI_VERSION; }
+
+int qsmd5_set_log_callback(qsmd5_log_fn fn, void* user) {
+  const LogSink* s = nullptr;
+  if (fn) {
+    s = new (std::nothrow) LogSink{fn, user};
+    if (!s) return fail(-ENOMEM, "qsmd5: host allocation failed");
+  }
+  g_log_sink.store(s, std::memory_order_release);
+  return 0;
+}
 
 int qsmd5_device_count(void) {
   if (g_forked_child.load(std::memory_order_relaxed)) return 0;  // the parent's HIP state
@@ -2289,6 +2411,7 @@ int qsmd5_get_stats(qsmd5_stats* out) {
   out->gpu_chunks = g_gpu_chunks.load();
   out->cpu_chunks = g_cpu_chunks.load();
   out->gpu_lost = g_gpu_lost.load() ? 1 : 0;
+  out->inits = g_inits.load();
   return 0;
 }
 
@@ -2345,6 +2468,7 @@ int qsmd5_ctx_create(qsmd5_ctx** out) {
 
 void qsmd5_ctx_destroy(qsmd5_ctx* c) {
   if (!c) return;
+  CallScope call;  // its device buffers are freed before a shutdown tears HIP down
   if (c->d_state) (void)hipFree(c->d_state);
   if (c->d_tail) (void)hipFree(c->d_tail);
   if (c->d_seg) (void)hipFree(c->d_seg);

@@ -50,10 +50,10 @@ class Stats(ctypes.Structure):
     _fields_ = [("gpu_batches", ctypes.c_uint64), ("cpu_batches", ctypes.c_uint64),
                 ("fallbacks", ctypes.c_uint64), ("gpu_chunks", ctypes.c_uint64),
                 ("cpu_chunks", ctypes.c_uint64), ("gpu_lost", ctypes.c_int),
-                ("reserved", ctypes.c_int)]
+                ("inits", ctypes.c_int)]
 
     def asdict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class Rates(ctypes.Structure):
@@ -80,6 +80,11 @@ class Part(ctypes.Structure):
 
 
 _lib = None
+
+# qsmd5_log_fn: void (*)(int level, const char* msg, void* user)
+LOG_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p)
+LOG_INFO, LOG_WARN, LOG_ERROR = 0, 1, 2  # qsfs LogLevel::Value (base/LogLevel.h:27)
+_log_keep = None  # the installed ctypes callback must outlive every call that may log
 
 
 def lib():
@@ -144,6 +149,7 @@ def lib():
         "qsmd5_synth_fill_lcg": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_uint32, ctypes.c_uint32,
                                                 ctypes.c_void_p]),
+        "qsmd5_set_log_callback": (ctypes.c_int, [LOG_FN, ctypes.c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -174,6 +180,19 @@ def shutdown():
     """qsmd5_shutdown: release the runtime's GPU resources (idempotent; a later
     call initialises afresh)."""
     _check(lib().qsmd5_shutdown(), "qsmd5_shutdown")
+
+
+def set_log_callback(fn):
+    """qsmd5_set_log_callback: route the library's messages to fn(level, text)
+    (level LOG_INFO / LOG_WARN / LOG_ERROR) instead of stderr; None restores
+    the default.  fn runs on the thread that made the qsmd5 call."""
+    global _log_keep
+    if fn is None:
+        _check(lib().qsmd5_set_log_callback(LOG_FN(), None), "qsmd5_set_log_callback")
+        return
+    cb = LOG_FN(lambda level, msg, _user: fn(level, msg.decode(errors="replace")))
+    _check(lib().qsmd5_set_log_callback(cb, None), "qsmd5_set_log_callback")
+    _log_keep = cb  # kept (never freed while set; a replaced one may still be running)
 
 
 def kernel_choice(n, flags=0):

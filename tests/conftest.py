@@ -33,6 +33,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "cpu_backend: exercises the library's CPU routing/fallback")
 
 
+# Host-sanitizer runs (test_gpu_sanitizers.py) are the slowest GPU tests and
+# the only ones that run uninstrumented vendor runtimes under TSan/ASan.  They
+# go last, so that under `-x` a failure there can never leave a parity test
+# unrun (round 3: a sanitizer child stopped the suite with 17 tests behind it).
+LAST_FILES = ("test_gpu_sanitizers.py",)
+
+
+def pytest_collection_modifyitems(session, config, items):
+    items.sort(key=lambda it: os.path.basename(str(it.fspath)) in LAST_FILES)  # stable
+
+
 def _ensure_built():
     """Build oracle/ and libqsmd5.so in place if a fresh checkout lacks them."""
     oracle_so = os.path.join(ROOT, "oracle", "libmd5_oracle.so")

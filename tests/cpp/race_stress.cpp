@@ -26,6 +26,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
 #include <thread>
 #include <vector>
@@ -76,6 +77,22 @@ uint32_t next(uint32_t& s) {
   return s;
 }
 
+// Every chunk a case builds must lie inside the worker's buffer.  Round 3's
+// negative control (max_len 64 KiB) built 128-256 KiB chunks in case 4 from a
+// 64 KiB buffer: `buf.size() - len + 1` wrapped, the chunk started up to 4 GiB
+// past the buffer, and the runtime's H2D copy of that pageable "chunk" read
+// unmapped TSan heap (GPUTEST_r03: SEGV, READ of 0x72c456febf4b).  Each range
+// is checked here before it is handed to the library.
+void in_buf(const std::vector<uint8_t>& buf, const void* p, size_t len, const char* what) {
+  const uint8_t* b = buf.data();
+  const uint8_t* q = static_cast<const uint8_t*>(p);
+  if (q < b || q > b + buf.size() || len > (size_t)(b + buf.size() - q)) {
+    fprintf(stderr, "race_stress bug: %s range [%p, +%zu) outside the %zu-byte buffer\n", what, p, len,
+            buf.size());
+    abort();
+  }
+}
+
 void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthreads) {
   std::vector<uint8_t> buf(max_len + 64);
   oracle_lcg_fill(buf.data(), buf.size(), 1000u + (uint32_t)t);
@@ -93,6 +110,7 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
     switch ((t + r) % 5) {
       case 0: {  // one part, pageable, arbitrary offset and length
         const size_t off = next(s) % 61, len = next(s) % (max_len - 64) + 1;
+        in_buf(buf, buf.data() + off, len, "hash_one");
         if ((rc = qsmd5_hash_one(buf.data() + off, len, d)) != 0) fail("hash_one", rc, t, r);
         else check(buf.data() + off, len, d, "hash_one", t, r);
         break;
@@ -102,11 +120,12 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
         std::vector<qsmd5_chunk> ch(n);
         std::vector<uint8_t> dg(16 * n);
         for (int i = 0; i < n; ++i) {
-          const size_t off = next(s) % 4099;
+          const size_t off = next(s) % std::min<size_t>(4099, buf.size());
           size_t len = i == 0 ? 0 : next(s) % (max_len / 4);
           if (off + len > buf.size()) len = buf.size() - off;
           ch[i].ptr = buf.data() + off;
           ch[i].len = len;
+          in_buf(buf, ch[i].ptr, len, "hash_batch");
         }
         rc = (r & 4) ? qsmd5_hash_batch_ex(ch.data(), n, (uint8_t(*)[16])dg.data(), QSMD5_FLAG_HOST)
                      : qsmd5_hash_batch(ch.data(), n, (uint8_t(*)[16])dg.data());
@@ -154,10 +173,15 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
         std::vector<qsmd5_chunk> ch(n);
         std::vector<uint8_t> dg(16 * n);
         for (int i = 0; i < n; ++i) {
-          const size_t len = i < 2 ? max_len / 4 + next(s) % 4096 : (128u << 10) + next(s) % (128u << 10);
+          // the short ones are 128-256 KiB at the default 3 MiB max_len;
+          // scaled down with smaller buffers, never longer than the buffer
+          const size_t lo = std::min<size_t>(128u << 10, max_len / 24 + 1);
+          size_t len = i < 2 ? max_len / 4 + next(s) % 4096 : lo + next(s) % lo;
+          len = std::min(len, buf.size());
           const size_t off = next(s) % (buf.size() - len + 1);
           ch[(i * 7) % n].ptr = buf.data() + off;  // long ones land mid-batch
           ch[(i * 7) % n].len = len;
+          in_buf(buf, ch[(i * 7) % n].ptr, len, "split batch");
         }
         if ((rc = qsmd5_hash_batch(ch.data(), n, (uint8_t(*)[16])dg.data())) != 0) fail("split batch", rc, t, r);
         else

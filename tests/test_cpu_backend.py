@@ -277,6 +277,45 @@ def test_log_names_the_backend(tmp_path):
     assert "qsmd5: backend=cpu reason=forced chunks=3 bytes=9" in out.stderr
 
 
+LOG_SINK_SCRIPT = r'''
+import ctypes, sys
+import qsmd5
+got = []
+qsmd5.set_log_callback(lambda level, msg: got.append((level, msg)))
+qsmd5.hash_batch([b"abc"] * 3, flags=qsmd5.FLAG_CPU_ONLY)
+if qsmd5.device_count() == 0:     # auto routing picks the GPU, which is absent here: fallback
+    big = (ctypes.c_uint8 * (10 << 20))()
+    qsmd5.hash_batch([(ctypes.addressof(big) + i * (256 << 10), 256 << 10) for i in range(40)])
+qsmd5.set_log_callback(None)
+qsmd5.hash_batch([b"x"], flags=qsmd5.FLAG_CPU_ONLY)   # not seen by the removed sink
+for level, msg in got:
+    print("%d|%s" % (level, msg))
+'''
+
+
+def test_log_callback_carries_backend_without_stderr():
+    """VERDICT r03 item 5 / SURVEY.md §5: qsmd5_set_log_callback hands each
+    call's backend, reason and size to the host's logger (qsfs: DebugInfo via
+    LogMacros.h) at LogLevel Info, and a GPU that cannot be used at Warn --
+    with nothing on stderr, even under QSMD5_LOG=1.  Removing the sink
+    restores stderr."""
+    env = dict(os.environ, QSMD5_LOG="1", QSMD5_BACKEND="auto",
+               PYTHONPATH=os.path.join(ROOT, "qsfs-fuse_amd"))
+    out = subprocess.run(["python", "-c", LOG_SINK_SCRIPT], env=env, capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    lines = [ln.split("|", 1) for ln in out.stdout.splitlines() if "|" in ln]
+    assert ["0", "qsmd5: backend=cpu reason=forced chunks=3 bytes=9"] in lines, out.stdout
+    # the removed sink saw nothing more; the default stderr logging is back
+    assert not any("chunks=1 bytes=1" in m for _, m in lines), out.stdout
+    assert "qsmd5: backend=cpu reason=forced chunks=1 bytes=1" in out.stderr
+    assert "chunks=3" not in out.stderr and "GPU" not in out.stderr, out.stderr
+    if qsmd5.device_count() == 0:
+        levels = {lvl for lvl, m in lines if "GPU" in m}
+        assert "1" in levels, out.stdout  # the unusable GPU and the fallback: LOG_WARN
+        assert any(m.startswith("qsmd5: backend=cpu reason=fallback chunks=40") for _, m in lines), out.stdout
+
+
 def test_product_library_does_not_carry_the_oracle():
     """The CPU backend is the library's own code: libqsmd5.so neither links
     the oracle nor exports or contains its symbols."""

@@ -100,6 +100,43 @@ print("child_ok=%s parent_ok=%s" % (child_ok, parent_ok))
 sys.exit(0 if child_ok and parent_ok else 1)
 '''
 
+FORK_AFTER_SHUTDOWN_SCRIPT = r'''
+import os, sys, signal
+import qsmd5
+L = qsmd5.lib()
+assert L.qsmd5_init(0) == 0
+assert qsmd5.hash_batch([b"abc"], flags=qsmd5.FLAG_GPU_ONLY)[0].hex() == "900150983cd24fb0d6963f7d28e17f72"
+assert L.qsmd5_shutdown() == 0                    # state back to "not initialised" ...
+inits = qsmd5.stats()["inits"]
+assert inits == 1, qsmd5.stats()
+pid = os.fork()                                   # ... and only then the fork
+if pid == 0:
+    signal.alarm(60)
+    try:
+        ok = L.qsmd5_init(0) == qsmd5.ENODEV
+        try:
+            qsmd5.hash_batch([b"abc"], flags=qsmd5.FLAG_GPU_ONLY)
+            ok = False
+        except qsmd5.Md5Error as e:
+            ok = ok and e.code == qsmd5.ENODEV
+        ok = ok and qsmd5.md5("message digest") == "f96b697d7cb7938d525a2f31aaf161d0"
+        ok = ok and L.qsmd5_shutdown() == 0 and L.qsmd5_init(0) == qsmd5.ENODEV
+        st = qsmd5.stats()
+        ok = ok and st["inits"] == inits          # no HIP initialisation ran in the child
+        if not ok:
+            print("child stats", st, file=sys.stderr)
+    except Exception as e:
+        print("child error", e, file=sys.stderr)
+        ok = False
+    os._exit(0 if ok else 3)
+_, st = os.waitpid(pid, 0)
+child_ok = os.WIFEXITED(st) and os.WEXITSTATUS(st) == 0
+parent_ok = qsmd5.hash_batch([b"a"], flags=qsmd5.FLAG_GPU_ONLY)[0].hex() == "0cc175b9c0f1b6a831c399e269772661"
+parent_ok = parent_ok and qsmd5.stats()["inits"] == 2     # the parent re-initialised
+print("child_ok=%s parent_ok=%s" % (child_ok, parent_ok))
+sys.exit(0 if child_ok and parent_ok else 1)
+'''
+
 WORKER_SCRIPT = r'''
 import sys, ctypes
 import qsmd5
@@ -153,6 +190,20 @@ def test_fork_after_init_child_hashes_on_cpu():
     call, auto routing hashes on the CPU, and the parent keeps its GPU."""
     env = dict(ENV, QSMD5_BACKEND="auto")
     out = subprocess.run([PY, "-c", FORK_AFTER_INIT_SCRIPT], env=env, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "child_ok=True parent_ok=True" in out.stdout
+
+
+@pytest.mark.cpu_backend
+def test_fork_after_shutdown_child_makes_no_hip_call():
+    """a child forked after the parent initialised AND shut the
+    runtime down still makes no HIP call: qsmd5_init, a GPU-only batch and a
+    re-init after the child's own shutdown return -ENODEV, the process's
+    initialisation count (qsmd5_stats.inits) stays where the fork left it,
+    and auto routing hashes on the CPU."""
+    env = dict(ENV, QSMD5_BACKEND="auto")
+    out = subprocess.run([PY, "-c", FORK_AFTER_SHUTDOWN_SCRIPT], env=env, capture_output=True,
                          text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "child_ok=True parent_ok=True" in out.stdout

@@ -16,7 +16,11 @@ batches split, and QSMD5_MAPS_AFTER=2 sends the classifier to its
 /proc/self/maps cache from the second pageable query.
 """
 import os
+import re
+import signal
 import subprocess
+import threading
+import time
 
 import pytest
 
@@ -25,6 +29,103 @@ from conftest import ROOT
 SAN = os.path.join(ROOT, "qsfs-fuse_amd", "lib", "san")
 REPORT_MARKERS = ("WARNING: ThreadSanitizer", "ERROR: AddressSanitizer", "runtime error:",
                   "ERROR: LeakSanitizer")
+
+
+SYMBOLIZER = "/opt/rocm/llvm/bin/llvm-symbolizer"
+
+
+class _Result:
+    def __init__(self, returncode, stdout, stderr):
+        self.returncode, self.stdout, self.stderr = returncode, stdout, stderr
+
+
+def _diagnose(pid, err):
+    """Where a sanitizer child that took a deadly signal is: the faulting pc and
+    address resolved against the child's own /proc/<pid>/maps (library, offset,
+    symbol), and what each of its threads is blocked in.  Read while the child
+    is still alive, so the layout is the one the fault happened in."""
+    lines = []
+    try:
+        with open("/proc/%d/maps" % pid) as f:
+            maps = [ln.split() for ln in f]
+    except OSError as e:
+        return "no maps: %s" % e
+    def find(addr):
+        for m in maps:
+            lo, hi = (int(x, 16) for x in m[0].split("-"))
+            if lo <= addr < hi:
+                return lo, m[5] if len(m) > 5 else "[anon]"
+        return None, None
+    for what, pat in (("pc", r"\(pc (0x[0-9a-f]+)"), ("address", r"on unknown address (0x[0-9a-f]+)")):
+        for hx in re.findall(pat, err):
+            a = int(hx, 16)
+            lo, path = find(a)
+            if path is None:
+                lines.append("%s %s: not mapped now" % (what, hx))
+                continue
+            base = min(int(m[0].split("-")[0], 16) for m in maps if len(m) > 5 and m[5] == path)
+            rel = a - base
+            sym = ""
+            if what == "pc" and path.startswith("/") and os.path.exists(SYMBOLIZER):
+                try:
+                    sym = subprocess.run([SYMBOLIZER, "--obj=" + path, hex(rel)], capture_output=True,
+                                         text=True, timeout=20).stdout.strip().replace("\n", " @ ")
+                except (OSError, subprocess.SubprocessError) as e:
+                    sym = "symbolizer: %s" % e
+            lines.append("%s %s: %s + %s %s" % (what, hx, path, hex(rel), sym))
+    try:
+        for tid in sorted(os.listdir("/proc/%d/task" % pid), key=int):
+            d = "/proc/%d/task/%s/" % (pid, tid)
+            def rd(name):
+                try:
+                    with open(d + name) as f:
+                        return f.read().strip()
+                except OSError:
+                    return "?"
+            lines.append("thread %s %-16s state %s wchan %s" % (tid, rd("comm"), rd("stat").split(") ")[-1][:1],
+                                                                rd("wchan")))
+    except OSError:
+        pass
+    return "\n".join(lines)
+
+
+def _watch(cmd, env, timeout=110, grace=15):
+    """subprocess.run with a watchdog: a child that reports a deadly signal
+    (a sanitizer's DEADLYSIGNAL) but does not exit within `grace` seconds, or
+    runs past `timeout`, is diagnosed (_diagnose) and killed with its process
+    group, and the test fails at once with its output -- one bad child costs
+    seconds, not the suite (round 3: a SEGV'd child hung to the 110 s limit)."""
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    bufs = {"out": [], "err": []}
+    readers = [threading.Thread(target=lambda f=f, k=k: bufs[k].extend(iter(f.readline, "")), daemon=True)
+               for f, k in ((p.stdout, "out"), (p.stderr, "err"))]
+    for r in readers:
+        r.start()
+    t0 = time.monotonic()
+    deadly_at = None
+    while p.poll() is None:
+        now = time.monotonic()
+        if deadly_at is None and any("DEADLYSIGNAL" in ln for ln in list(bufs["err"])):
+            deadly_at = now
+        if (deadly_at is not None and now - deadly_at > grace) or now - t0 > timeout:
+            err = "".join(bufs["err"])
+            diag = _diagnose(p.pid, err)
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except OSError:
+                pass
+            p.wait()
+            for r in readers:
+                r.join(5)
+            why = "took a deadly signal and did not exit within %d s" % grace if deadly_at is not None \
+                else "ran past %d s" % timeout
+            pytest.fail("%s %s; killed.\n--- diagnosis ---\n%s\n--- stderr ---\n%s\n--- stdout ---\n%s" % (
+                os.path.basename(cmd[0]), why, diag, "".join(bufs["err"])[-6000:], "".join(bufs["out"])[-2000:]))
+        time.sleep(0.1)
+    for r in readers:
+        r.join(10)
+    return _Result(p.returncode, "".join(bufs["out"]), "".join(bufs["err"]))
 
 
 def _run(variant, devices, threads=6, rounds=12, max_len=3 << 20, extra=(), expect_clean=True,
@@ -53,8 +154,7 @@ def _run(variant, devices, threads=6, rounds=12, max_len=3 << 20, extra=(), expe
     env["ASAN_OPTIONS"] = "detect_leaks=0:abort_on_error=0:exitcode=23"
     env["TSAN_OPTIONS"] = ("halt_on_error=0:exitcode=66:second_deadlock_stack=1:print_suppressions=1:"
                            "suppressions=" + os.path.join(ROOT, "tests", "cpp", "tsan_hip.supp"))
-    out = subprocess.run([exe, str(threads), str(rounds), str(max_len)] + list(extra), env=env,
-                         capture_output=True, text=True, timeout=110)
+    out = _watch([exe, str(threads), str(rounds), str(max_len)] + list(extra), env)
     text = out.stdout + out.stderr
     if not expect_clean:
         return out.returncode, text
@@ -96,6 +196,16 @@ def test_race_stress_auto_backend(variant, inject):
     print(out)
     assert "backend=gpu+cpu reason=split" in out, out[-3000:]
     assert "backend=cpu reason=size" in out, out[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", ["tsan", "asan"])
+def test_race_stress_small_buffers(variant):
+    """The negative control's sizes (64 KiB buffers) without the planted race:
+    every case's chunks stay inside the worker's buffer (race_stress.cpp
+    in_buf aborts otherwise), under both sanitizers.  Round 3's control built
+    128-256 KiB chunks from a 64 KiB buffer and hashed unmapped memory."""
+    print(_run(variant, "", threads=4, rounds=10, max_len=1 << 16))
 
 
 @pytest.mark.gpu

@@ -251,3 +251,44 @@ def test_register_buffers_sharing_a_page():
             qsmd5.unregister_host(b)
     finally:
         qsmd5.unregister_host(a)
+
+
+@pytest.mark.parametrize("column", [None, 1024])
+def test_shared_page_survives_unregistering_its_first_owner(column):
+    """two registrations share a boundary page; the FIRST one (a)
+    is unregistered while the second (b) is still registered, and b -- whose
+    first page is the shared one -- is then hashed through the gather kernel
+    (a 16-B-aligned row in a registered allocation of its own) against the
+    oracle, before b is unregistered too.  A page unpinned or unmapped with a
+    would fault the gather kernel or hash stale bytes here."""
+    blk = np.zeros(128 * 4096, dtype=np.uint8)
+    blk[:] = np.random.default_rng(78).integers(0, 256, size=blk.size, dtype=np.uint8)
+    base = (blk.ctypes.data + 4095) & ~4095
+    a, la = base + 96, 2 * 4096 - 96 - 1024       # ends inside page 1, at a 16-B boundary
+    b, lb = a + la, 100 * 4096 + 1000             # starts in page 1, right after a; with the
+    #                                               other rows > 256 KiB: staged, not inline
+    assert b % 16 == 0
+    qsmd5.register_host(a, la)
+    try:
+        qsmd5.register_host(b, lb)
+    except qsmd5.Md5Error as e:
+        qsmd5.unregister_host(a)
+        pytest.skip("HIP refused the shared-page registration (-EINVAL path): %s" % e)
+    a_done = False
+    try:
+        qsmd5.unregister_host(a)
+        a_done = True
+        other = qsmd5.alloc_pinned(1 << 16)       # a second row in its own allocation
+        try:
+            _fill_n(other, 1 << 16, 79)
+            chunks = [(b, lb), (other, 5000), (b + 16, lb - 16)]
+            for _ in range(2):
+                _check(chunks, column=column)
+            blk[b - base:b - base + 64] ^= 0x5a  # the shared page changes: no stale copy
+            _check(chunks, column=column)
+        finally:
+            qsmd5.free_pinned(other)
+    finally:
+        qsmd5.unregister_host(b)
+        if not a_done:
+            qsmd5.unregister_host(a)
