@@ -3,29 +3,52 @@
 //
 // The reference uploads a file's parts in QSTransferManager::DoMultiPartUpload
 // (src/client/QSTransferManager.cpp:602-673): for each queued part it acquires
-// a pooled transfer buffer (ResourceManager::Acquire, ResourceManager.cpp:54-70),
-// gathers the part's bytes from the file's pages into it (File::ReadNoLoad,
-// src/data/File.cpp:308-375), wraps it in an IOStream of the part's size, and
-// hands it to UploadMultipart, which computes md5(stream) for the
-// Content-MD5 (QSClient.cpp:369-371): one buffer, one serial hash, at a time.
+// a pooled transfer buffer (ResourceManager::Acquire, ResourceManager.cpp:53-67,
+// which BLOCKS until a buffer is free), gathers the part's bytes from the
+// file's pages into it (File::ReadNoLoad, src/data/File.cpp:308-375), wraps it
+// in an IOStream of the part's size, and hands it to UploadMultipart, which
+// computes md5(stream) for the Content-MD5 (QSClient.cpp:369-371).  The buffer
+// goes back to the pool when the part's upload returns
+// (ReceivedHandlerMultipleUpload, QSTransferManager.cpp:215-220).  One buffer,
+// one serial hash, at a time; a flushing thread never holds more than one
+// buffer while it waits for another.
 //
-// upload_parts_prehashed() keeps that loop and its buffer discipline but
-// hashes in waves: it gathers as many parts as the pool has buffers, hashes the
-// whole wave with ONE qsmd5_hash_batch_ex(QSMD5_FLAG_HOST) call (pool buffers
-// are host memory), then hands each part, its buffer and its hex digest to the
-// uploader.  The library routes the wave by size (QSMD5_BACKEND=auto): a
-// default qsfs pool (50 MiB of 10 MiB buffers = 5, configure/Default.cpp:157,
-// TransferManager.cpp:78-84) is below the GPU break-even and hashes on the CPU;
-// a larger pool (-Z) or a whole flushed file goes to the gfx950 kernels.
+// upload_parts_prehashed() keeps that buffer discipline and hashes in waves:
+//   - a wave blocks in acquire() for its FIRST buffer only, while it holds no
+//     buffer of its own, and then takes just the buffers free at that moment
+//     (try_acquire(), which never blocks).  So no thread ever waits for a
+//     buffer while holding one that only it would release, and any number of
+//     files flushing at once through one blocking pool cannot deadlock (the
+//     hold-and-wait condition never holds);
+//   - the wave's parts are gathered (read) and hashed with ONE
+//     qsmd5_hash_batch_ex(QSMD5_FLAG_HOST) call, routed by size like any call
+//     (few parts: the library's CPU MD5; many: the gfx950 kernels);
+//   - each part, its buffer and its hex digest go to the caller's upload,
+//     and the buffer is released as soon as that part's upload returns;
+//   - with `pipeline` (default), the next wave is gathered and hashed on a
+//     helper thread while this thread uploads the current one, so the hash
+//     time hides behind the upload (the overlap the reference's async
+//     handler has, QSTransferManager.cpp:654-659).
+//
+// The pool holds `-n` (numtransfer) buffers of `-b` MiB: the transfer
+// manager's heap is bufSize x maxParallelTransfers (TransferManager.h:74-86,
+// constructed with defaults at Drive.cpp:124), shared by every file upload.
+// Waves are therefore at most -n parts: qsfs's default -n 5 keeps them below
+// the GPU break-even (about 25 parts of 10 MiB at the default 4 CPU threads)
+// and on the CPU; -n 32 or more sends full waves to the GPU.
 //
 // Header-only over the C-ABI (include/qsmd5.h).  Throws qsmd5::Error on a
-// hashing failure and std::runtime_error on a short read, as the reference
-// stops the upload there (QSTransferManager.cpp:622-643).
+// hashing failure and std::runtime_error on a short read or a shut-down pool,
+// as the reference stops the upload there (QSTransferManager.cpp:611-643).
 #ifndef QSFS_AMD_QSFS_MULTIPART_HPP_
 #define QSFS_AMD_QSFS_MULTIPART_HPP_
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <exception>
+#include <future>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -78,64 +101,262 @@ class BufferSlab {
   std::vector<char> heap_;
 };
 
-// What one wave did: parts hashed, and which backend the library picked.
+// The pool interface upload_parts_prehashed needs -- ResourceManager's
+// Acquire / Release (ResourceManager.cpp:53-77) plus a non-blocking
+// try_acquire -- restated over PoolBuffers.  A qsfs binding adapts the real
+// ResourceManager instead; any type with the same members
+// works:
+//   typedef ... buffer_type;                       copyable handle
+//   buffer_type acquire();                         blocks; a null handle = shut down
+//   bool try_acquire(buffer_type* out);            never blocks; false = none free
+//   void release(const buffer_type& b);
+//   static char* data(const buffer_type& b);       nullptr for a null handle
+//   static size_t size(const buffer_type& b);
+class BlockingPool {
+ public:
+  typedef PoolBuffer buffer_type;
+  explicit BlockingPool(std::vector<PoolBuffer> buffers) : free_(std::move(buffers)) {}
+  buffer_type acquire() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return shutdown_ || !free_.empty(); });
+    if (shutdown_) return PoolBuffer{nullptr, 0};
+    const PoolBuffer b = free_.back();
+    free_.pop_back();
+    return b;
+  }
+  bool try_acquire(buffer_type* out) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (shutdown_ || free_.empty()) return false;
+    *out = free_.back();
+    free_.pop_back();
+    return true;
+  }
+  void release(const buffer_type& b) {
+    if (!b.data) return;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      free_.push_back(b);
+    }
+    cv_.notify_one();
+  }
+  void shutdown() {  // ResourceManager::ShutdownAndWait's flag: acquire() stops blocking
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      shutdown_ = true;
+    }
+    cv_.notify_all();
+  }
+  size_t free_count() {
+    std::lock_guard<std::mutex> lk(mu_);
+    return free_.size();
+  }
+  static char* data(const buffer_type& b) { return b.data; }
+  static size_t size(const buffer_type& b) { return b.size; }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<PoolBuffer> free_;
+  bool shutdown_ = false;
+};
+
+// What the upload did: parts hashed, which backend the library picked for
+// each wave, and the time in each phase.  gather_s and hash_s are summed over
+// waves wherever they ran (with `pipeline`, mostly on the helper thread,
+// overlapped with upload_s); wait_s is the time the uploading thread spent
+// waiting for the next wave to be ready, i.e. hashing NOT hidden.
 struct WaveStats {
   size_t waves = 0, parts = 0;
   size_t gpu_waves = 0, cpu_waves = 0, split_waves = 0;  // by qsmd5_last_backend of each wave
-  double gather_s = 0, hash_s = 0, upload_s = 0;  // wall time in each phase
+  size_t widest_wave = 0;
+  double gather_s = 0, hash_s = 0, upload_s = 0, wait_s = 0, wall_s = 0;
 };
 
-// parts:    the file's parts as PrepareUpload slices them (qsmd5_plan_parts).
-// pool:     the transfer buffers, each at least the largest part.
-// read:     read(part, char* buf) -> bytes gathered (File::ReadNoLoad).
-// upload:   upload(part, const char* buf, const std::string& hex) hands the part
-//           on (UploadMultipart with SetContentMD5(hex)); the buffer may be
-//           reused once it returns.
-template <class Read, class Upload>
-WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts,
-                                 const std::vector<PoolBuffer>& pool, Read&& read,
-                                 Upload&& upload) {
-  if (pool.empty() && !parts.empty()) throw std::invalid_argument("empty buffer pool");
-  WaveStats st;
-  std::vector<qsmd5_chunk> chunks;
+struct PrehashOptions {
+  bool pipeline = true;        // gather + hash the next wave while this one uploads
+  size_t max_wave = 0;         // parts per wave at most (0: as many as free buffers)
+  bool upload_releases = false;  // true: upload() owns each buffer and releases it to
+                                 // the pool itself (an async executor's completion
+                                 // handler); false: released when upload() returns
+};
+
+namespace detail {
+
+template <class Pool>
+struct Wave {
+  size_t first = 0;  // index of its first part
+  std::vector<typename Pool::buffer_type> bufs;
   std::vector<uint8_t> dig;
-  for (size_t first = 0; first < parts.size(); first += pool.size()) {
-    using clock = std::chrono::steady_clock;
-    auto secs = [](clock::time_point a, clock::time_point b) {
-      return std::chrono::duration<double>(b - a).count();
-    };
+  int backend = 0;
+  double gather_s = 0, hash_s = 0;
+};
+
+template <class Pool>
+void release_all(Pool& pool, std::vector<typename Pool::buffer_type>& bufs, size_t from = 0) {
+  for (size_t k = from; k < bufs.size(); ++k) pool.release(bufs[k]);
+  bufs.resize(std::min(from, bufs.size()));
+}
+
+// Take the buffers of the wave starting at part `first` (block for one while
+// holding none, then only what is free), gather its parts, hash them.  On any
+// failure every buffer it took is back in the pool before it throws.
+// keep_half: the first wave of a pipelined upload keeps half of the buffers
+// it could get and gives the rest back at once, so that the next wave (on the
+// helper thread) has buffers to fill while this one uploads: the pool's
+// buffers then alternate between the wave in upload and the wave in hashing.
+template <class Pool, class Read>
+Wave<Pool> prepare_wave(const std::vector<qsmd5_part>& parts, size_t first, Pool& pool, Read& read,
+                        size_t max_wave, bool keep_half) {
+  using clock = std::chrono::steady_clock;
+  Wave<Pool> w;
+  w.first = first;
+  const size_t want = std::min(max_wave ? max_wave : parts.size(), parts.size() - first);
+  typename Pool::buffer_type b = pool.acquire();
+  if (!Pool::data(b)) throw std::runtime_error("transfer buffer pool is shut down: upload stopped");
+  try {
+    w.bufs.push_back(b);
+    while (w.bufs.size() < want && pool.try_acquire(&b)) w.bufs.push_back(b);
+    if (keep_half && w.bufs.size() < parts.size() - first) release_all(pool, w.bufs, (w.bufs.size() + 1) / 2);
+    const size_t n = w.bufs.size();
     const auto t0 = clock::now();
-    const size_t n = std::min(pool.size(), parts.size() - first);
-    chunks.resize(n);
+    std::vector<qsmd5_chunk> chunks(n);
     for (size_t k = 0; k < n; ++k) {
       const qsmd5_part& p = parts[first + k];
-      if (pool[k].size < p.size) throw std::invalid_argument("pool buffer smaller than a part");
-      const size_t got = read(p, pool[k].data);
+      if (Pool::size(w.bufs[k]) < p.size) throw std::invalid_argument("pool buffer smaller than a part");
+      const size_t got = read(p, Pool::data(w.bufs[k]));
       if (got != p.size)
         throw std::runtime_error("short read of part " + std::to_string(p.part_number) + ": " +
                                  std::to_string(got) + " of " + std::to_string(p.size) + " bytes");
-      chunks[k] = qsmd5_chunk{pool[k].data, p.size};
+      chunks[k] = qsmd5_chunk{Pool::data(w.bufs[k]), p.size};
     }
     const auto t1 = clock::now();
-    dig.resize(16 * n);
-    detail::check(qsmd5_hash_batch_ex(chunks.data(), n, reinterpret_cast<uint8_t(*)[16]>(dig.data()),
-                                      QSMD5_FLAG_HOST),
-                  "qsmd5_hash_batch_ex");
+    w.dig.resize(16 * n);
+    check(qsmd5_hash_batch_ex(chunks.data(), n, reinterpret_cast<uint8_t(*)[16]>(w.dig.data()),
+                              QSMD5_FLAG_HOST),
+          "qsmd5_hash_batch_ex");
+    w.backend = qsmd5_last_backend();  // this thread's call
+    w.gather_s = std::chrono::duration<double>(t1 - t0).count();
+    w.hash_s = std::chrono::duration<double>(clock::now() - t1).count();
+  } catch (...) {
+    release_all(pool, w.bufs);
+    throw;
+  }
+  return w;
+}
+
+}  // namespace detail
+
+// parts:    the file's parts as PrepareUpload slices them (qsmd5_plan_parts).
+// pool:     the transfer buffer pool (see BlockingPool for the members used),
+//           each buffer at least the largest part; shared with other uploads.
+// read:     read(part, char* buf) -> bytes gathered (File::ReadNoLoad).  With
+//           `pipeline` it runs on a helper thread, one wave at a time.
+// upload:   upload(part, const buffer_type& buf, const std::string& hex) hands
+//           the part on (UploadMultipart with SetContentMD5(hex)), on the
+//           calling thread, in part order.  Unless opt.upload_releases, the
+//           buffer goes back to the pool when it returns (or throws).
+template <class Pool, class Read, class Upload>
+WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& pool, Read&& read,
+                                 Upload&& upload, const PrehashOptions& opt = PrehashOptions()) {
+  using clock = std::chrono::steady_clock;
+  typedef detail::Wave<Pool> W;
+  WaveStats st;
+  const auto t_start = clock::now();
+  if (parts.empty()) return st;
+  auto secs = [](clock::time_point a, clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+  };
+  auto prep = [&](size_t first) {
+    return detail::prepare_wave(parts, first, pool, read, opt.max_wave, opt.pipeline && first == 0);
+  };
+  std::future<W> ahead;  // the next wave, being prepared on the helper thread
+  // On the way out after a failure: the wave in preparation finishes (its
+  // thread may be waiting for a buffer this thread just released), and its
+  // buffers go back to the pool.
+  auto drain_ahead = [&]() noexcept {
+    if (!ahead.valid()) return;
+    try {
+      W w = ahead.get();
+      detail::release_all(pool, w.bufs);
+    } catch (...) {
+    }
+  };
+  W cur = prep(0);
+  for (;;) {
+    const size_t n = cur.bufs.size(), next = cur.first + n;
     ++st.waves;
     st.parts += n;
-    switch (qsmd5_last_backend()) {
+    st.widest_wave = std::max(st.widest_wave, n);
+    st.gather_s += cur.gather_s;
+    st.hash_s += cur.hash_s;
+    switch (cur.backend) {
       case QSMD5_BACKEND_GPU: ++st.gpu_waves; break;
       case QSMD5_BACKEND_SPLIT: ++st.split_waves; break;  // longest parts on the CPU, the rest on the GPU
       default: ++st.cpu_waves; break;
     }
-    const auto t2 = clock::now();
-    for (size_t k = 0; k < n; ++k) upload(parts[first + k], pool[k].data, detail::hex(&dig[16 * k]));
-    const auto t3 = clock::now();
-    st.gather_s += secs(t0, t1);
-    st.hash_s += secs(t1, t2);
-    st.upload_s += secs(t2, t3);
+    if (opt.pipeline && next < parts.size()) {
+      try {
+        ahead = std::async(std::launch::async, prep, next);
+      } catch (const std::system_error&) {
+        // no thread to spare: this wave uploads, then the next is prepared here
+      }
+    }
+    const auto t0 = clock::now();
+    size_t k = 0;
+    try {
+      for (; k < n; ++k) {
+        const qsmd5_part& p = parts[cur.first + k];
+        const std::string hex = detail::hex(&cur.dig[16 * k]);
+        if (opt.upload_releases) {
+          const typename Pool::buffer_type b = cur.bufs[k];
+          cur.bufs[k] = typename Pool::buffer_type();  // owned by upload() from here
+          upload(p, b, hex);
+        } else {
+          try {
+            upload(p, cur.bufs[k], hex);
+          } catch (...) {
+            pool.release(cur.bufs[k]);
+            cur.bufs[k] = typename Pool::buffer_type();
+            throw;
+          }
+          pool.release(cur.bufs[k]);  // ReceivedHandlerMultipleUpload: back to the pool
+          cur.bufs[k] = typename Pool::buffer_type();
+        }
+      }
+    } catch (...) {
+      detail::release_all(pool, cur.bufs, k + 1);  // parts of this wave never handed over
+      drain_ahead();
+      throw;
+    }
+    const auto t1 = clock::now();
+    st.upload_s += secs(t0, t1);
+    if (next >= parts.size()) break;
+    if (ahead.valid()) {
+      cur = ahead.get();  // rethrows the helper's failure (its buffers are already back)
+      st.wait_s += secs(t1, clock::now());
+    } else {
+      cur = prep(next);
+      st.wait_s += secs(t1, clock::now());
+    }
   }
+  st.wall_s = secs(t_start, clock::now());
   return st;
+}
+
+// The vector-of-buffers form: `pool` is this upload's own set of buffers
+// (a BlockingPool over them), and upload(part, const char* buf, hex) returns
+// when the part is sent.
+template <class Read, class Upload>
+WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts,
+                                 const std::vector<PoolBuffer>& buffers, Read&& read, Upload&& upload,
+                                 const PrehashOptions& opt = PrehashOptions()) {
+  if (buffers.empty() && !parts.empty()) throw std::invalid_argument("empty buffer pool");
+  BlockingPool pool(buffers);
+  PrehashOptions o = opt;
+  o.upload_releases = false;
+  return upload_parts_prehashed(
+      parts, pool, read,
+      [&](const qsmd5_part& p, const PoolBuffer& b, const std::string& hex) { upload(p, b.data, hex); }, o);
 }
 
 }  // namespace qsmd5

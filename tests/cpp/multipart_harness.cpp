@@ -7,33 +7,51 @@
 // Then it runs the reference's upload loop through the drop-in helper
 // qsmd5::upload_parts_prehashed (qsfs-fuse_amd/host/qsfs_multipart.hpp):
 //   - parts sliced as PrepareUpload does (qsmd5_plan_parts, QSTransferManager.cpp:475-550);
-//   - a pool of transfer buffers (ResourceManager; default 5 x 10 MiB);
+//   - a blocking pool of transfer buffers (ResourceManager, ResourceManager.cpp:53-77:
+//     -n buffers of -b MiB, TransferManager.h:74-86; qsfs's default is 5 x 10 MiB);
 //   - each part gathered from the pages into a pool buffer by a ReadNoLoad
 //     restatement (File.cpp:308-375: the pages intersecting [off, off + len),
 //     copied piece by piece; bytes no page holds are a short read);
-//   - one qsmd5_hash_batch_ex(QSMD5_FLAG_HOST) per wave of pool-size parts;
+//   - one qsmd5_hash_batch_ex(QSMD5_FLAG_HOST) per wave;
 //   - each part's hex digest handed to the "uploader" (UploadMultipart's
-//     SetContentMD5, QSClient.cpp:369-371), which records it.
+//     SetContentMD5, QSClient.cpp:369-371), which records it, optionally after
+//     a simulated network time (--upload-ms), on this thread (the reference's
+//     sync path, File::Flush -> UploadFile(async = false)) or on an executor
+//     (--async=E threads: its async path, QSTransferManager.cpp:654-659).
+// --files=F flushes F files at once from F threads through ONE shared pool,
+// as qsfs's FUSE threads do; a watchdog reports a deadlock (every waiter
+// blocked and no pool or upload progress for --deadlock-s seconds) and exits
+// with status 3.  --naive-wave=W replaces the helper with the hold-and-wait
+// flow round 3's INTEGRATION.md sketched (W blocking Acquire calls before the
+// wave is hashed): the negative control that deadlocks under the same load.
 // File content: part-aligned mode (--aligned) makes part i = LCG(12345 + i),
-// the parts of tests/golden/batch_10MiB.json; otherwise the file is one
-// LCG(seed) stream.  Prints one JSON object with the digests in part order
-// and where the time went (the last pass; hash_s_runs lists every pass's hash
-// time); tests/test_gpu_multipart.py and
+// the parts of tests/golden/batch_10MiB.json, for every file; otherwise file f
+// is one LCG(seed + f) stream.  Prints one JSON object with the digests in
+// part order and where the time went; tests/test_gpu_multipart.py and
 // tests/test_multipart_cpu.py check the digests.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <unistd.h>
 
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../qsfs-fuse_amd/host/qsfs_multipart.hpp"
 
 namespace {
+
+using clock_type = std::chrono::steady_clock;
 
 void lcg(uint32_t seed, uint8_t* out, uint64_t n) {
   uint32_t x = seed;
@@ -69,15 +87,178 @@ struct PagedFile {
   }
 };
 
+void build_file(PagedFile* file, uint64_t size, bool aligned, uint64_t buf, uint32_t seed) {
+  file->size = size;
+  std::vector<uint8_t> all(size);
+  if (aligned) {
+    for (uint64_t p = 0; p * buf < size; ++p)
+      lcg(12345u + (uint32_t)p, all.data() + p * buf, std::min(buf, size - p * buf));
+  } else {
+    lcg(seed, all.data(), size);
+  }
+  std::mt19937_64 rng(seed);
+  for (uint64_t off = 0; off < size;) {
+    const uint64_t len = std::min<uint64_t>(size - off, 1024 + rng() % (3u << 20));
+    file->pages.emplace(off, std::vector<char>(all.begin() + off, all.begin() + off + len));
+    off += len;
+  }
+}
+
+std::atomic<int64_t> g_progress_ns{0};  // last pool or upload event (watchdog)
+void progress() {
+  g_progress_ns.store(clock_type::now().time_since_epoch().count(), std::memory_order_relaxed);
+}
+
+// ResourceManager restated with a watchdog's view: BlockingPool (blocking
+// acquire, try_acquire, release) plus a count of threads blocked in acquire.
+class WatchedPool {
+ public:
+  typedef qsmd5::PoolBuffer buffer_type;
+  explicit WatchedPool(std::vector<qsmd5::PoolBuffer> b) : pool_(std::move(b)) {}
+  buffer_type acquire() {
+    buffer_type b;
+    if (pool_.try_acquire(&b)) {
+      progress();
+      return b;
+    }
+    waiting_.fetch_add(1);
+    b = pool_.acquire();
+    waiting_.fetch_sub(1);
+    progress();
+    return b;
+  }
+  bool try_acquire(buffer_type* out) {
+    const bool ok = pool_.try_acquire(out);
+    if (ok) progress();
+    return ok;
+  }
+  void release(const buffer_type& b) {
+    pool_.release(b);
+    if (b.data) progress();
+  }
+  void shutdown() { pool_.shutdown(); }
+  int waiting() const { return waiting_.load(); }
+  size_t free_count() { return pool_.free_count(); }
+  static char* data(const buffer_type& b) { return b.data; }
+  static size_t size(const buffer_type& b) { return b.size; }
+
+ private:
+  qsmd5::BlockingPool pool_;
+  std::atomic<int> waiting_{0};
+};
+
+// The transfer manager's executor (ThreadPool, TransferManager.cpp:55-60):
+// E threads running submitted upload tasks in order.
+class Executor {
+ public:
+  explicit Executor(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~Executor() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+        if (q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
+  std::vector<std::thread> th_;
+  bool stop_ = false;
+};
+
+// Parts of one file still being uploaded on the executor.
+struct InFlight {
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t n = 0;
+  void add() {
+    std::lock_guard<std::mutex> lk(mu);
+    ++n;
+  }
+  void done() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      --n;
+    }
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [&] { return n == 0; });
+  }
+};
+
+void sleep_ms(double ms) {
+  if (ms > 0) std::this_thread::sleep_for(std::chrono::duration<double, std::milli>(ms));
+}
+
+// The hold-and-wait flow (negative control): W blocking acquires, one part
+// gathered after each, before the wave is hashed and uploaded.
+qsmd5::WaveStats naive_upload(const std::vector<qsmd5_part>& parts, WatchedPool& pool,
+                              const PagedFile& file, size_t W, double upload_ms,
+                              std::vector<std::string>* md5) {
+  qsmd5::WaveStats st;
+  for (size_t first = 0; first < parts.size(); first += W) {
+    const size_t n = std::min(W, parts.size() - first);
+    std::vector<qsmd5::PoolBuffer> held;
+    std::vector<qsmd5_chunk> ch;
+    for (size_t k = 0; k < n; ++k) {
+      held.push_back(pool.acquire());  // blocks while holding the buffers taken so far
+      const qsmd5_part& p = parts[first + k];
+      file.read(p.offset, p.size, held.back().data);
+      ch.push_back(qsmd5_chunk{held.back().data, p.size});
+      sleep_ms(1);
+    }
+    std::vector<uint8_t> dig(16 * n);
+    qsmd5::detail::check(qsmd5_hash_batch_ex(ch.data(), n, reinterpret_cast<uint8_t(*)[16]>(dig.data()),
+                                             QSMD5_FLAG_HOST),
+                         "qsmd5_hash_batch_ex");
+    for (size_t k = 0; k < n; ++k) {
+      sleep_ms(upload_ms);
+      (*md5)[parts[first + k].part_number - 1] = qsmd5::detail::hex(&dig[16 * k]);
+      pool.release(held[k]);
+    }
+    ++st.waves;
+    st.parts += n;
+  }
+  return st;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   uint64_t size = 64ull * 10 * 1024 * 1024;
-  size_t pool_n = 5;
-  bool aligned = false, pinned = false, slab = false, reg = false;
+  size_t pool_n = 5, files = 1, naive_wave = 0, max_wave = 0;
+  bool aligned = false, pinned = false, slab = false, reg = false, pipeline = true;
   uint32_t seed = 12345;
   uint64_t buf = 10ull << 20;
-  int repeat = 1;
+  int repeat = 1, async_threads = 0;
+  double upload_ms = 0, deadlock_s = 20;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&](const char* key) { return a.rfind(key, 0) == 0 ? a.c_str() + strlen(key) : nullptr; };
@@ -86,33 +267,30 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--seed=")) seed = (uint32_t)strtoul(v, nullptr, 0);
     else if (const char* v = val("--buf=")) buf = strtoull(v, nullptr, 0);
     else if (const char* v = val("--repeat=")) repeat = std::max(1, atoi(v));
+    else if (const char* v = val("--files=")) files = std::max<size_t>(1, strtoull(v, nullptr, 0));
+    else if (const char* v = val("--upload-ms=")) upload_ms = atof(v);
+    else if (const char* v = val("--async=")) async_threads = atoi(v);
+    else if (const char* v = val("--naive-wave=")) naive_wave = strtoull(v, nullptr, 0);
+    else if (const char* v = val("--max-wave=")) max_wave = strtoull(v, nullptr, 0);
+    else if (const char* v = val("--deadlock-s=")) deadlock_s = atof(v);
     else if (a == "--aligned") aligned = true;
     else if (a == "--pinned") pinned = true;
     else if (a == "--slab") slab = true;
     else if (a == "--register") reg = true;
+    else if (a == "--no-pipeline") pipeline = false;
     else {
       fprintf(stderr, "unknown argument %s\n", argv[i]);
       return 2;
     }
   }
-  // The file's bytes, cut into pages of 1 KiB .. 3 MiB.
-  PagedFile file;
-  file.size = size;
-  {
-    std::vector<uint8_t> all(size);
-    if (aligned) {
-      for (uint64_t p = 0; p * buf < size; ++p)
-        lcg(12345u + (uint32_t)p, all.data() + p * buf, std::min(buf, size - p * buf));
-    } else {
-      lcg(seed, all.data(), size);
-    }
-    std::mt19937_64 rng(seed);
-    for (uint64_t off = 0; off < size;) {
-      const uint64_t len = std::min<uint64_t>(size - off, 1024 + rng() % (3u << 20));
-      file.pages.emplace(off, std::vector<char>(all.begin() + off, all.begin() + off + len));
-      off += len;
-    }
+  if (pool_n < 1) {
+    fprintf(stderr, "--pool must be >= 1\n");
+    return 2;
   }
+  // The files' bytes, cut into pages of 1 KiB .. 3 MiB (aligned: one shared
+  // file, every part golden; otherwise file f = LCG(seed + f)).
+  std::vector<PagedFile> file(aligned ? 1 : files);
+  for (size_t f = 0; f < file.size(); ++f) build_file(&file[f], size, aligned, buf, seed + (uint32_t)f);
   size_t n = 0;
   if (qsmd5_plan_parts(size, buf, 4ull << 20, 20ull << 20, 0, nullptr, 0, &n)) return 1;
   std::vector<qsmd5_part> parts(n);
@@ -147,12 +325,11 @@ int main(int argc, char** argv) {
       pool.push_back({owned.back()->data(), largest});
     }
   }
-  std::vector<std::string> md5(n);
   (void)qsmd5_init(0);  // runtime start-up outside the timed uploads (-ENODEV without a GPU)
   // --register: lock the pageable pool's pages once, as a daemon would at start-up
   double register_s = 0;
   if (reg && !pinned) {
-    const auto r0 = std::chrono::steady_clock::now();
+    const auto r0 = clock_type::now();
     // one registration per allocation: the slab at once, else each buffer
     std::vector<qsmd5::PoolBuffer> regs =
         slab ? std::vector<qsmd5::PoolBuffer>{{slab_pool->data(), slab_pool->bytes()}} : pool;
@@ -161,27 +338,87 @@ int main(int argc, char** argv) {
         fprintf(stderr, "qsmd5_register_host: %s\n", qsmd5_last_error());
         return 1;
       }
-    register_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - r0).count();
+    register_s = std::chrono::duration<double>(clock_type::now() - r0).count();
   }
-  // --repeat: upload the file again through the same pool, as a daemon reuses
+  WatchedPool shared(pool);
+  std::unique_ptr<Executor> exec(async_threads > 0 ? new Executor(async_threads) : nullptr);
+  // Watchdog: a thread blocked in acquire, and nothing moved for deadlock_s.
+  std::atomic<bool> finished{false};
+  progress();
+  std::thread watchdog([&] {
+    while (!finished.load()) {
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+      const double idle = (clock_type::now().time_since_epoch().count() - g_progress_ns.load()) * 1e-9;
+      if (shared.waiting() > 0 && idle > deadlock_s) {
+        printf("{\"deadlock\": true, \"waiting\": %d, \"free\": %zu, \"idle_s\": %.1f}\n", shared.waiting(),
+               shared.free_count(), idle);
+        fflush(stdout);
+        fprintf(stderr, "deadlock: %d thread(s) blocked in acquire, %zu buffer(s) free, no progress "
+                "for %.1f s\n", shared.waiting(), shared.free_count(), idle);
+        _exit(3);
+      }
+    }
+  });
+  // --repeat: upload the files again through the same pool, as a daemon reuses
   // its buffers; the first pass pays HIP's first-touch locking of pageable pages.
-  std::vector<double> hash_runs;
-  qsmd5::WaveStats st;
+  std::vector<std::vector<std::string>> md5(files, std::vector<std::string>(n));
+  std::vector<double> hash_runs, wall_runs;
+  std::vector<qsmd5::WaveStats> st(files);
+  std::vector<std::string> errors(files);
   double total = 0;
   for (int rep = 0; rep < repeat; ++rep) {
-    const auto t0 = std::chrono::steady_clock::now();
-    try {
-      st = qsmd5::upload_parts_prehashed(
-          parts, pool,
-          [&](const qsmd5_part& p, char* dst) { return file.read(p.offset, p.size, dst); },
-          [&](const qsmd5_part& p, const char*, const std::string& hex) { md5[p.part_number - 1] = hex; });
-    } catch (const std::exception& e) {
-      fprintf(stderr, "upload failed: %s\n", e.what());
+    const auto t0 = clock_type::now();
+    std::vector<std::thread> th;
+    for (size_t f = 0; f < files; ++f) {
+      th.emplace_back([&, f] {
+        const PagedFile& pf = file[aligned ? 0 : f];
+        try {
+          if (naive_wave) {
+            st[f] = naive_upload(parts, shared, pf, naive_wave, upload_ms, &md5[f]);
+            return;
+          }
+          qsmd5::PrehashOptions opt;
+          opt.pipeline = pipeline;
+          opt.max_wave = max_wave;
+          opt.upload_releases = exec != nullptr;
+          InFlight inflight;
+          auto read = [&](const qsmd5_part& p, char* dst) { return pf.read(p.offset, p.size, dst); };
+          auto upload = [&](const qsmd5_part& p, const qsmd5::PoolBuffer& b, const std::string& hex) {
+            if (!exec) {  // sync: UploadMultipart on this thread, the buffer released after it
+              sleep_ms(upload_ms);
+              md5[f][p.part_number - 1] = hex;
+              progress();
+              return;
+            }
+            inflight.add();  // async: the executor uploads, its handler releases the buffer
+            exec->submit([&, p, b, hex] {
+              sleep_ms(upload_ms);
+              md5[f][p.part_number - 1] = hex;
+              shared.release(b);
+              inflight.done();
+            });
+          };
+          st[f] = qsmd5::upload_parts_prehashed(parts, shared, read, upload, opt);
+          inflight.wait();
+        } catch (const std::exception& e) {
+          errors[f] = e.what();
+        }
+      });
+    }
+    for (auto& t : th) t.join();
+    total = std::chrono::duration<double>(clock_type::now() - t0).count();
+    double h = 0;
+    for (auto& s : st) h += s.hash_s;
+    hash_runs.push_back(h);
+    wall_runs.push_back(total);
+  }
+  finished.store(true);
+  watchdog.join();
+  for (size_t f = 0; f < files; ++f)
+    if (!errors[f].empty()) {
+      fprintf(stderr, "upload of file %zu failed: %s\n", f, errors[f].c_str());
       return 1;
     }
-    total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    hash_runs.push_back(st.hash_s);
-  }
   if (pinned && !slab)
     for (auto& b : pool) qsmd5_free_pinned(b.data);
   if (reg && !pinned) {
@@ -189,17 +426,41 @@ int main(int argc, char** argv) {
     else
       for (auto& b : pool) qsmd5_unregister_host(b.data);
   }
-  printf("{\"size\": %llu, \"parts\": %zu, \"pages\": %zu, \"pool\": %zu, \"pinned\": %s, "
-         "\"slab\": %s, \"registered\": %s, \"register_s\": %.6f, \"waves\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"split_waves\": %zu, \"seconds\": %.6f, "
-         "\"gather_s\": %.6f, \"hash_s\": %.6f, \"upload_s\": %.6f, \"part_sizes\": [",
-         (unsigned long long)size, n, file.pages.size(), pool_n, pinned ? "true" : "false",
-         slab ? "true" : "false", reg && !pinned ? "true" : "false", register_s, st.waves,
-         st.gpu_waves, st.cpu_waves, st.split_waves, total, st.gather_s, st.hash_s, st.upload_s);
+  qsmd5::WaveStats sum;
+  for (const auto& s : st) {
+    sum.waves += s.waves;
+    sum.parts += s.parts;
+    sum.gpu_waves += s.gpu_waves;
+    sum.cpu_waves += s.cpu_waves;
+    sum.split_waves += s.split_waves;
+    sum.widest_wave = std::max(sum.widest_wave, s.widest_wave);
+    sum.gather_s += s.gather_s;
+    sum.hash_s += s.hash_s;
+    sum.upload_s += s.upload_s;
+    sum.wait_s += s.wait_s;
+  }
+  auto md5_list = [&](const std::vector<std::string>& v) {
+    std::string s = "[";
+    for (size_t i = 0; i < v.size(); ++i) s += std::string(i ? ", " : "") + "\"" + v[i] + "\"";
+    return s + "]";
+  };
+  printf("{\"deadlock\": false, \"size\": %llu, \"parts\": %zu, \"files\": %zu, \"pages\": %zu, \"pool\": %zu, "
+         "\"pinned\": %s, \"slab\": %s, \"registered\": %s, \"pipeline\": %s, \"async_threads\": %d, "
+         "\"naive_wave\": %zu, \"upload_ms\": %.3f, \"register_s\": %.6f, \"waves\": %zu, "
+         "\"widest_wave\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"split_waves\": %zu, "
+         "\"seconds\": %.6f, \"gather_s\": %.6f, \"hash_s\": %.6f, \"upload_s\": %.6f, \"wait_s\": %.6f, "
+         "\"part_sizes\": [",
+         (unsigned long long)size, n, files, file[0].pages.size(), pool_n, pinned ? "true" : "false",
+         slab ? "true" : "false", reg && !pinned ? "true" : "false", pipeline ? "true" : "false",
+         async_threads, naive_wave, upload_ms, register_s, sum.waves, sum.widest_wave, sum.gpu_waves,
+         sum.cpu_waves, sum.split_waves, total, sum.gather_s, sum.hash_s, sum.upload_s, sum.wait_s);
   for (size_t i = 0; i < n; ++i) printf("%s%llu", i ? ", " : "", (unsigned long long)parts[i].size);
   printf("], \"hash_s_runs\": [");
   for (size_t i = 0; i < hash_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", hash_runs[i]);
-  printf("], \"md5\": [");
-  for (size_t i = 0; i < n; ++i) printf("%s\"%s\"", i ? ", " : "", md5[i].c_str());
+  printf("], \"wall_s_runs\": [");
+  for (size_t i = 0; i < wall_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", wall_runs[i]);
+  printf("], \"md5\": %s, \"md5_files\": [", md5_list(md5[0]).c_str());
+  for (size_t f = 0; f < files; ++f) printf("%s%s", f ? ", " : "", md5_list(md5[f]).c_str());
   printf("]}\n");
   return 0;
 }

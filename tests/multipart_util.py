@@ -15,16 +15,20 @@ def build():
         subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", src,
                                "-I" + os.path.join(ROOT, "include"),
                                "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
-                               "-Wl,-rpath,$ORIGIN/../../qsfs-fuse_amd/lib", "-o", HARNESS])
+                               "-lpthread", "-Wl,-rpath,$ORIGIN/../../qsfs-fuse_amd/lib", "-o", HARNESS])
 
 
-def run(args, backend, timeout=300, extra_env=None):
+def run_raw(args, backend, timeout=300, extra_env=None):
     build()
     env = dict(os.environ, QSMD5_BACKEND=backend)
     env.update(extra_env or {})
-    out = subprocess.run([HARNESS] + list(args), env=env, capture_output=True, text=True,
-                         timeout=timeout)
-    assert out.returncode == 0, out.stderr[-3000:]
+    return subprocess.run([HARNESS] + list(args), env=env, capture_output=True, text=True,
+                          timeout=timeout)
+
+
+def run(args, backend, timeout=300, extra_env=None):
+    out = run_raw(args, backend, timeout, extra_env)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
     r = json.loads(out.stdout)
     r["_stderr"] = out.stderr
     return r

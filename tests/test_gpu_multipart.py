@@ -34,7 +34,7 @@ def test_whole_file_wave_on_the_gpu(gold, pinned, slab):
     """A pool as large as the file: one wave, one GPU batch of 512 parts, from
     pool buffers allocated one by one (as ResourceManager does) or carved from
     one slab (qsmd5::BufferSlab), pageable or pinned."""
-    args = ["--aligned", "--size=%d" % (512 * 10 * MiB), "--pool=512", "--repeat=3"]
+    args = ["--aligned", "--size=%d" % (512 * 10 * MiB), "--pool=512", "--repeat=3", "--no-pipeline"]
     args += (["--pinned"] if pinned else []) + (["--slab"] if slab else [])
     r = run(args, "gpu")
     assert r["parts"] == 512 and r["waves"] == 1 and r["gpu_waves"] == 1
@@ -52,9 +52,9 @@ def test_default_pool_routes_waves_by_size(gold):
     """auto: qsfs's default pool (5 x 10 MiB buffers, 50 MiB heap) gives waves
     below the GPU break-even, hashed on the CPU; a 64-buffer pool's waves go to
     the gfx950 kernels.  Same golden digests either way."""
-    small = run(["--aligned", "--size=%d" % (64 * 10 * MiB), "--pool=5"], "auto")
+    small = run(["--aligned", "--size=%d" % (64 * 10 * MiB), "--pool=5", "--no-pipeline"], "auto")
     assert small["waves"] == 13 and small["cpu_waves"] == 13 and small["gpu_waves"] == 0
-    big = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=64"], "auto")
+    big = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=64", "--no-pipeline"], "auto")
     assert big["waves"] == 2 and big["gpu_waves"] == 2
     assert small["md5"] == gold[:64] and big["md5"] == gold[:128]
     print("64 parts, pool 5 (CPU waves): hash %.3f s; 128 parts, pool 64 (GPU waves): hash %.3f s"
@@ -66,8 +66,8 @@ def test_registered_pageable_pool(gold):
     """qsfs's own pageable buffers, registered once (qsmd5_register_host, as
     at daemon start-up): no first-touch page locking, and the separate buffers'
     rows go through the gather kernel."""
-    r = run(["--aligned", "--size=%d" % (512 * 10 * MiB), "--pool=512", "--register", "--repeat=2"],
-            "gpu")
+    r = run(["--aligned", "--size=%d" % (512 * 10 * MiB), "--pool=512", "--register", "--repeat=2",
+             "--no-pipeline"], "gpu")
     assert r["registered"] and r["gpu_waves"] == 1
     assert r["md5"] == gold[:512]
     first, warm = r["hash_s_runs"]
@@ -86,7 +86,7 @@ def test_pool_refilled_between_waves(gold, pool_kind):
     host data served from a GPU-side cache would repeat wave 1's digests in
     wave 2; every digest must be part k's own."""
     flag = "--pinned" if pool_kind == "pinned" else "--register"
-    r = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=64", flag, "--repeat=2"], "gpu",
+    r = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=64", flag, "--repeat=2", "--no-pipeline"], "gpu",
             extra_env={"QSMD5_TRACE": "1"})
     assert r["parts"] == 128 and r["waves"] == 2 and r["gpu_waves"] == 2
     assert r["md5"] == gold[:128]

@@ -9,8 +9,10 @@ import ctypes
 import json
 import os
 
+import pytest
+
 from conftest import GOLDEN
-from multipart_util import run
+from multipart_util import run, run_raw
 from oracle_util import lcg_bytes, md5_many
 
 MiB = 1 << 20
@@ -18,7 +20,7 @@ MiB = 1 << 20
 
 def test_aligned_parts_match_golden():
     gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
-    r = run(["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5"], "cpu")
+    r = run(["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5", "--no-pipeline"], "cpu")
     assert r["parts"] == 12 and r["waves"] == 3 and r["cpu_waves"] == 3
     assert r["md5"] == gold[:12]
 
@@ -36,3 +38,60 @@ def test_prepare_upload_slicing_and_ragged_tail():
             off += L
         assert off == size
         assert r["md5"] == [d.hex() for d in md5_many(want)], size
+
+
+@pytest.mark.parametrize("mode", ["sync", "sync_no_pipeline", "async_executor"])
+def test_concurrent_files_share_a_blocking_pool(mode):
+    """four files of 12 parts flush at once from four
+    threads through ONE blocking 5-buffer pool (ResourceManager::Acquire
+    blocks, ResourceManager.cpp:53-67), with a simulated 2 ms upload per part:
+    on the caller's thread (the reference's sync path), or on a 3-thread
+    executor whose completion handler releases the buffer (its async path,
+    QSTransferManager.cpp:654-659).  A wave only ever blocks for its first
+    buffer while holding none, so no deadlock (the harness's watchdog would
+    exit 3), and every part of every file matches the golden table."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    args = ["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5", "--files=4", "--upload-ms=2",
+            "--deadlock-s=10"]
+    if mode == "sync_no_pipeline":
+        args.append("--no-pipeline")
+    if mode == "async_executor":
+        args.append("--async=3")
+    r = run(args, "cpu", timeout=120)
+    assert r["deadlock"] is False and r["files"] == 4 and r["parts"] == 12
+    assert r["widest_wave"] <= 5 and r["waves"] >= 4 * 3
+    for f, got in enumerate(r["md5_files"]):
+        assert got == gold[:12], f
+
+
+def test_hold_and_wait_flow_deadlocks():
+    """The negative control for the test above: the flow round 3's
+    INTEGRATION.md sketched -- blocking Acquire per part of a 4-part wave
+    before hashing it -- under the same four files and 5-buffer pool holds
+    buffers while it waits for more, and the harness's watchdog finds every
+    uploader blocked with no buffer free (exit 3)."""
+    out = run_raw(["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5", "--files=4",
+                   "--naive-wave=4", "--deadlock-s=3"], "cpu", timeout=120)
+    assert out.returncode == 3, out.stdout + out.stderr
+    r = json.loads(out.stdout.splitlines()[-1])
+    assert r["deadlock"] is True and r["free"] == 0 and r["waiting"] >= 2
+
+
+def test_pipeline_hides_hashing_behind_upload():
+    """with the pipeline, the next wave is gathered and
+    hashed on a helper thread while this thread uploads (20 ms per part
+    simulated), so the uploader hardly waits for hashing (wait_s); without it
+    every wave's gather + hash sits between uploads.  Same golden digests."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    base = ["--aligned", "--size=%d" % (24 * 10 * MiB), "--pool=8", "--upload-ms=20"]
+    serial = run(base + ["--no-pipeline"], "cpu", timeout=120)
+    piped = run(base, "cpu", timeout=120)
+    assert serial["md5"] == gold[:24] and piped["md5"] == gold[:24]
+    # the first wave is hashed before any upload can start, in both
+    first = piped["seconds"] - piped["upload_s"] - piped["wait_s"]
+    print("serial: wall %.3f s, upload %.3f s, waiting for hashes %.3f s; pipelined: wall %.3f s, "
+          "upload %.3f s, waiting %.3f s (first wave %.3f s)"
+          % (serial["seconds"], serial["upload_s"], serial["wait_s"], piped["seconds"],
+             piped["upload_s"], piped["wait_s"], first))
+    assert piped["wait_s"] < 0.3 * serial["wait_s"], (piped, serial)
+    assert piped["seconds"] < serial["seconds"]
