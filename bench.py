@@ -233,7 +233,7 @@ def config5_host_leg(args, rank, world, dev, cpu=False):
     import torch
     import torch.distributed as dist
     from bench_config5 import HostShard, L as PART
-    from qsmd5.parallel import shard_range
+    from qsmd5.parallel import group_report
 
     dist_on = dist.is_initialized()
     want = args.config5_parts
@@ -273,26 +273,29 @@ def config5_host_leg(args, rank, world, dev, cpu=False):
         return {"skipped": "a rank could not hold its shard of %d parts in pinned host memory%s"
                            % (n, (": " + err) if err else "")}, True
     sync = (lambda: None) if cpu else torch.cuda.synchronize
-    for _ in range(args.config5_warmup):
-        shard.step()
     reps = max(1, args.config5_reps)
-    if dist_on:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    table = None
-    for _ in range(reps):
-        table = shard.step()
-    sync()
-    if dist_on:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist_on:
-        tt = torch.tensor([elapsed], dtype=torch.float64,
-                          device="cpu" if cpu or dist.get_backend() == "gloo" else dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-    shard.close()
+    with shard:  # the pinned shard is freed whatever happens below
+        for _ in range(args.config5_warmup):
+            shard.step()
+        if dist_on:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        table = None
+        for _ in range(reps):
+            table = shard.step()
+        sync()
+        if dist_on:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if dist_on:
+            tt = torch.tensor([elapsed], dtype=torch.float64,
+                              device="cpu" if cpu or dist.get_backend() == "gloo" else dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            elapsed = float(tt.item())
+        pg = group_report(shard.m, None if cpu else dev) if dist_on else None
+        path = shard.path
+        m_local = shard.m
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_10MiB.json")))["md5"]
     got = [bytes(r).hex() for r in table.cpu().numpy()]
     ok = n <= len(gold) and got == gold[:n]
@@ -304,14 +307,14 @@ def config5_host_leg(args, rank, world, dev, cpu=False):
                     "memory, qsmd5_hash_batch_ex(QSMD5_FLAG_HOST) over its own GPU link, "
                     "16-B digest all-gather inside the timed region" % (n, n * PART / 2.0 ** 30),
         "value": round(value, 3), "unit": "GiB/s", "scaling": "strong", "n_gpus": world,
-        "parts": n, "parts_per_rank": [shard_range(n, r, world)[1] - shard_range(n, r, world)[0]
-                                       for r in range(world)],
+        "parts": n, "parts_per_rank": [x["parts"] for x in pg["ranks"]] if pg else [m_local],
         "seconds_per_pass": round(per_pass, 4), "passes": reps, "warmup": args.config5_warmup,
         "per_gpu_GiBps": round(value / world, 3),
         "collective": ("RCCL all_gather_into_tensor (16 B per part)"
                        if dist_on and dist.get_backend() == "nccl" else
                        "gloo all_gather (host)" if dist_on else "none (one rank)"),
-        "path": shard.path,
+        "process_group": pg,
+        "path": path,
         "parity": "ok: %d/%d digests == reference golden" % (n, n) if ok else "FAIL",
     }
     if n != want:
@@ -350,7 +353,7 @@ def main():
     import torch
     import torch.distributed as dist
     import qsmd5
-    from qsmd5.parallel import gather_digests
+    from qsmd5.parallel import gather_digests, group_report
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -371,6 +374,9 @@ def main():
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        # from here the group, not the launcher's environment, says how many
+        # ranks there are
+        world, rank = dist.get_world_size(), dist.get_rank()
     rc = qsmd5.lib().qsmd5_init(0)
     if rc != 0:
         raise SystemExit("qsmd5_init failed: %d" % rc)
@@ -437,6 +443,7 @@ def main():
         bad = [i for i in range(min(ntot, len(gold))) if got_hex[i] != gold[i]]
         log("PARITY FAILURE: %d of %d digests differ (first %s)" % (len(bad), ntot, bad[:5]))
 
+    pg = group_report(B, dev) if distributed else None
     job_bytes = float(ntot) * L
     value = job_bytes / (1 << 30) / elapsed * args.steps
     ms_per_step = elapsed / args.steps * 1e3
@@ -486,6 +493,7 @@ def main():
                       "note": "MD5 is a serial chain per chunk; at batch=512 the job rate is "
                               "512 x the per-chain rate (SURVEY.md §0 item 5)"},
         "parity": "ok: %d/%d digests == reference golden" % (ntot, ntot) if parity_ok else "FAIL",
+        "process_group": pg,
         "cpu_baseline": None,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -520,6 +528,7 @@ def cpu_rehearsal(args):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29517")
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    world, rank = dist.get_world_size(), dist.get_rank()
     c5, ok = config5_host_leg(args, rank, world, torch.device("cpu"), cpu=True)
     if rank == 0:
         print(json.dumps({"rehearsal": "cpu ranks over gloo, libqsmd5 CPU backend (no GPU; not "

@@ -43,3 +43,38 @@ def gather_digests(local, n, group=None):
         dist.all_gather_into_tensor(out, pad, group=group)
     rows = [out[r * m_max: r * m_max + (e - b)] for r, (b, e) in enumerate(sizes)]
     return torch.cat(rows, 0)
+
+
+def group_report(parts_local, device=None, group=None):
+    """What the process group itself says about a multi-rank run: its backend
+    and size (dist.get_backend / get_world_size, not the launcher's
+    environment) and, all-gathered from every rank, that rank's GPU (ordinal
+    and PCI domain:bus:device; -1 on CPU ranks) and the parts it hashed.  A
+    scaling line carrying this shows RCCL saw N ranks on N distinct GPUs."""
+    world = dist.get_world_size(group)
+    backend = dist.get_backend(group)
+    ordinal, pci = -1, (-1, -1, -1)
+    if device is not None and getattr(device, "type", "cpu") == "cuda":
+        ordinal = device.index if device.index is not None else torch.cuda.current_device()
+        p = torch.cuda.get_device_properties(ordinal)
+        pci = (getattr(p, "pci_domain_id", -1), getattr(p, "pci_bus_id", -1),
+               getattr(p, "pci_device_id", -1))
+    mine = torch.tensor([dist.get_rank(group), ordinal, pci[0], pci[1], pci[2], int(parts_local)],
+                        dtype=torch.int64)
+    if backend == "gloo":
+        rows = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(rows, mine, group=group)
+    else:
+        mine = mine.to(device)
+        out = torch.empty((world, mine.numel()), dtype=torch.int64, device=device)
+        dist.all_gather_into_tensor(out, mine.reshape(1, -1), group=group)
+        rows = list(out.cpu())
+    ranks = []
+    for r in rows:
+        rank, dev, dom, bus, slot, parts = (int(x) for x in r.tolist())
+        ranks.append({"rank": rank, "device": dev,
+                      "pci": "%04x:%02x:%02x" % (dom, bus, slot) if bus >= 0 else None,
+                      "parts": parts})
+    pcis = {x["pci"] for x in ranks if x["pci"]}
+    return {"backend": backend, "world_size": world, "ranks": ranks,
+            "distinct_gpus": len(pcis)}

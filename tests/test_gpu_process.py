@@ -233,6 +233,9 @@ def test_bench_two_rank_rehearsal():
     assert r["cpu_baseline"] is None and r["scaling"] == "weak"
     c5 = r["config5_host"]
     assert c5["parts_per_rank"] == [20, 20] and c5["parity"] == "ok: 40/40 digests == reference golden"
+    pg = r["process_group"]  # the group's own account: two gloo ranks sharing one card
+    assert pg["backend"] == "gloo" and pg["world_size"] == 2 and pg["distinct_gpus"] == 1
+    assert [x["parts"] for x in pg["ranks"]] == [64, 64] and {x["device"] for x in pg["ranks"]} == {0}
 
 
 def test_bench_rehearsal_rank_without_parts():
@@ -274,3 +277,7 @@ def test_bench_rccl_path_world_one():
     assert r["parity"].startswith("ok: 64/64")
     c5 = r["config5_host"]
     assert c5["collective"].startswith("RCCL") and c5["parity"] == "ok: 32/32 digests == reference golden"
+    for pg in (r["process_group"], c5["process_group"]):  # RCCL's own world, over its own GPU
+        assert pg["backend"] == "nccl" and pg["world_size"] == 1 and pg["distinct_gpus"] == 1
+        assert pg["ranks"][0]["pci"] is not None
+    assert r["process_group"]["ranks"][0]["parts"] == 64 and c5["process_group"]["ranks"][0]["parts"] == 32
