@@ -34,8 +34,10 @@
 // manager's heap is bufSize x maxParallelTransfers (TransferManager.h:74-86,
 // constructed with defaults at Drive.cpp:124), shared by every file upload.
 // Waves are therefore at most -n parts: qsfs's default -n 5 keeps them below
-// the GPU break-even (about 25 parts of 10 MiB at the default 4 CPU threads)
-// and on the CPU; -n 32 or more sends full waves to the GPU.
+// the GPU break-even and on the CPU; on the MI355X box auto routing first
+// sends waves to the GPU at -n 64 (the break-even, priced at the host's
+// measured CPU rate, lies between 33 and 64 parts of 10 MiB there;
+// INTEGRATION.md §3, profiles/r04_pool_sweep.jsonl).
 //
 // Header-only over the C-ABI (include/qsmd5.h).  Throws qsmd5::Error on a
 // hashing failure and std::runtime_error on a short read or a shut-down pool,
