@@ -201,10 +201,10 @@ struct InFlight {
     ++n;
   }
   void done() {
-    {
-      std::lock_guard<std::mutex> lk(mu);
-      --n;
-    }
+    // notify under the lock: the waiter may destroy this object as soon as it
+    // sees n == 0 (TSan caught the notify racing the destructor)
+    std::lock_guard<std::mutex> lk(mu);
+    --n;
     cv.notify_all();
   }
   void wait() {

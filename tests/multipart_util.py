@@ -32,3 +32,22 @@ def run(args, backend, timeout=300, extra_env=None):
     r = json.loads(out.stdout)
     r["_stderr"] = out.stderr
     return r
+
+
+HARNESS_TSAN = os.path.join(ROOT, "tests", "cpp", "multipart_harness_tsan")
+
+
+def build_tsan():
+    """The harness and the drop-in header (qsfs_multipart.hpp: helper thread,
+    pool, executor handoff) under ThreadSanitizer; libqsmd5 itself is not
+    instrumented (its own threads are covered by test_gpu_sanitizers.py)."""
+    src = os.path.join(ROOT, "tests", "cpp", "multipart_harness.cpp")
+    hdr = os.path.join(ROOT, "qsfs-fuse_amd", "host", "qsfs_multipart.hpp")
+    newest = max(os.path.getmtime(src), os.path.getmtime(hdr))
+    if not os.path.exists(HARNESS_TSAN) or os.path.getmtime(HARNESS_TSAN) < newest:
+        subprocess.check_call(["/opt/rocm/llvm/bin/clang++", "-std=c++17", "-O1", "-g",
+                               "-fsanitize=thread", src, "-I" + os.path.join(ROOT, "include"),
+                               "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
+                               "-lpthread", "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"),
+                               "-o", HARNESS_TSAN])
+    return HARNESS_TSAN

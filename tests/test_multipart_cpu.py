@@ -12,7 +12,9 @@ import os
 import pytest
 
 from conftest import GOLDEN
-from multipart_util import run, run_raw
+import subprocess
+
+from multipart_util import build_tsan, run, run_raw
 from oracle_util import lcg_bytes, md5_many
 
 MiB = 1 << 20
@@ -95,3 +97,22 @@ def test_pipeline_hides_hashing_behind_upload():
              piped["upload_s"], piped["wait_s"], first))
     assert piped["wait_s"] < 0.3 * serial["wait_s"], (piped, serial)
     assert piped["seconds"] < serial["seconds"]
+
+
+@pytest.mark.parametrize("mode", [[], ["--async=3"], ["--no-pipeline"], ["--max-wave=2"]],
+                         ids=["sync", "async", "no_pipeline", "max_wave_2"])
+def test_concurrent_files_under_tsan(mode):
+    """The drop-in header's threads -- the pipeline's helper thread preparing
+    the next wave, the shared pool, the executor's completion handler
+    releasing buffers -- under ThreadSanitizer, four files at once through
+    one 5-buffer pool: no report, every digest golden."""
+    exe = build_tsan()
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    env = dict(os.environ, QSMD5_BACKEND="cpu", TSAN_OPTIONS="halt_on_error=0:exitcode=66")
+    out = subprocess.run(["setarch", "x86_64", "-R", exe, "--aligned", "--size=%d" % (12 * 10 * MiB),
+                          "--pool=5", "--files=4", "--upload-ms=2", "--deadlock-s=20"] + mode,
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-8000:]
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads(out.stdout)
+    assert r["deadlock"] is False and all(m == gold[:12] for m in r["md5_files"])
