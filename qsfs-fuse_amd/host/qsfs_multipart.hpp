@@ -177,9 +177,9 @@ struct WaveStats {
 struct PrehashOptions {
   bool pipeline = true;        // gather + hash the next wave while this one uploads
   size_t max_wave = 0;         // parts per wave at most (0: as many as free buffers)
-  bool upload_releases = false;  // true: upload() owns each buffer and releases it to
-                                 // the pool itself (an async executor's completion
-                                 // handler); false: released when upload() returns
+  bool upload_releases = false;  // true: a buffer is upload()'s once upload() returns, and
+                                 // its completion handler releases it (an async
+                                 // executor); false: released when upload() returns
 };
 
 namespace detail {
@@ -255,8 +255,10 @@ Wave<Pool> prepare_wave(const std::vector<qsmd5_part>& parts, size_t first, Pool
 //           `pipeline` it runs on a helper thread, one wave at a time.
 // upload:   upload(part, const buffer_type& buf, const std::string& hex) hands
 //           the part on (UploadMultipart with SetContentMD5(hex)), on the
-//           calling thread, in part order.  Unless opt.upload_releases, the
-//           buffer goes back to the pool when it returns (or throws).
+//           calling thread, in part order.  If it throws, the buffer goes back
+//           to the pool and the upload stops there.  If it returns: with
+//           opt.upload_releases the buffer is now upload()'s, whose completion
+//           handler releases it; otherwise it goes back to the pool at once.
 template <class Pool, class Read, class Upload>
 WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& pool, Read&& read,
                                  Upload&& upload, const PrehashOptions& opt = PrehashOptions()) {
@@ -309,21 +311,18 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
       for (; k < n; ++k) {
         const qsmd5_part& p = parts[cur.first + k];
         const std::string hex = detail::hex(&cur.dig[16 * k]);
-        if (opt.upload_releases) {
-          const typename Pool::buffer_type b = cur.bufs[k];
-          cur.bufs[k] = typename Pool::buffer_type();  // owned by upload() from here
-          upload(p, b, hex);
-        } else {
-          try {
-            upload(p, cur.bufs[k], hex);
-          } catch (...) {
-            pool.release(cur.bufs[k]);
-            cur.bufs[k] = typename Pool::buffer_type();
-            throw;
-          }
-          pool.release(cur.bufs[k]);  // ReceivedHandlerMultipleUpload: back to the pool
+        // A buffer is upload()'s once upload() returns (upload_releases: its
+        // completion handler releases it); if upload() throws, it was not
+        // taken and goes back to the pool here.
+        try {
+          upload(p, cur.bufs[k], hex);
+        } catch (...) {
+          pool.release(cur.bufs[k]);
           cur.bufs[k] = typename Pool::buffer_type();
+          throw;
         }
+        if (!opt.upload_releases) pool.release(cur.bufs[k]);  // ReceivedHandlerMultipleUpload
+        cur.bufs[k] = typename Pool::buffer_type();
       }
     } catch (...) {
       detail::release_all(pool, cur.bufs, k + 1);  // parts of this wave never handed over

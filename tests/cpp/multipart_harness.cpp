@@ -274,6 +274,7 @@ int main(int argc, char** argv) {
   uint64_t buf = 10ull << 20;
   int repeat = 1, async_threads = 0;
   double upload_ms = 0, deadlock_s = 20;
+  uint32_t short_read_part = 0, fail_upload_part = 0;  // fault injection (1-based part numbers)
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&](const char* key) { return a.rfind(key, 0) == 0 ? a.c_str() + strlen(key) : nullptr; };
@@ -288,6 +289,8 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--naive-wave=")) naive_wave = strtoull(v, nullptr, 0);
     else if (const char* v = val("--max-wave=")) max_wave = strtoull(v, nullptr, 0);
     else if (const char* v = val("--deadlock-s=")) deadlock_s = atof(v);
+    else if (const char* v = val("--short-read-part=")) short_read_part = (uint32_t)strtoul(v, nullptr, 0);
+    else if (const char* v = val("--fail-upload-part=")) fail_upload_part = (uint32_t)strtoul(v, nullptr, 0);
     else if (a == "--aligned") aligned = true;
     else if (a == "--pinned") pinned = true;
     else if (a == "--slab") slab = true;
@@ -398,8 +401,12 @@ int main(int argc, char** argv) {
           opt.max_wave = max_wave;
           opt.upload_releases = exec != nullptr;
           InFlight inflight;
-          auto read = [&](const qsmd5_part& p, char* dst) { return pf.read(p.offset, p.size, dst); };
+          auto read = [&](const qsmd5_part& p, char* dst) {
+            const size_t got = pf.read(p.offset, p.size, dst);
+            return p.part_number == short_read_part ? got / 2 : got;  // File::ReadNoLoad found a hole
+          };
           auto upload = [&](const qsmd5_part& p, const qsmd5::PoolBuffer& b, const std::string& hex) {
+            if (p.part_number == fail_upload_part) throw std::runtime_error("injected upload failure");
             if (!exec) {  // sync: UploadMultipart on this thread, the buffer released after it
               sleep_ms(upload_ms);
               md5[f][p.part_number - 1] = hex;
@@ -431,11 +438,18 @@ int main(int argc, char** argv) {
   }
   finished.store(true);
   watchdog.join();
+  const bool injected = short_read_part || fail_upload_part;
   for (size_t f = 0; f < files; ++f)
     if (!errors[f].empty()) {
       fprintf(stderr, "upload of file %zu failed: %s\n", f, errors[f].c_str());
-      return 1;
+      if (!injected) return 1;
     }
+  // After an injected failure: which parts reached the uploader, and whether
+  // every buffer is back in the pool (nothing leaked by the helper thread).
+  size_t uploaded = 0;
+  for (const auto& v : md5)
+    for (const auto& h : v) uploaded += !h.empty();
+  const size_t pool_free_after = shared.free_count();
   if (pinned && !slab)
     for (auto& b : pool) qsmd5_free_pinned(b.data);
   if (reg && !pinned) {
@@ -461,13 +475,13 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < v.size(); ++i) s += std::string(i ? ", " : "") + "\"" + v[i] + "\"";
     return s + "]";
   };
-  printf("{\"deadlock\": false, \"size\": %llu, \"parts\": %zu, \"files\": %zu, \"pages\": %zu, \"pool\": %zu, "
+  printf("{\"deadlock\": false, \"error\": \"%s\", \"uploaded\": %zu, \"pool_free_after\": %zu, \"size\": %llu, \"parts\": %zu, \"files\": %zu, \"pages\": %zu, \"pool\": %zu, "
          "\"pinned\": %s, \"slab\": %s, \"registered\": %s, \"pipeline\": %s, \"async_threads\": %d, "
          "\"naive_wave\": %zu, \"upload_ms\": %.3f, \"register_s\": %.6f, \"waves\": %zu, "
          "\"widest_wave\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"split_waves\": %zu, "
          "\"seconds\": %.6f, \"gather_s\": %.6f, \"hash_s\": %.6f, \"upload_s\": %.6f, \"wait_s\": %.6f, "
          "\"part_sizes\": [",
-         (unsigned long long)size, n, files, file[0].pages.size(), pool_n, pinned ? "true" : "false",
+         errors[0].c_str(), uploaded, pool_free_after, (unsigned long long)size, n, files, file[0].pages.size(), pool_n, pinned ? "true" : "false",
          slab ? "true" : "false", reg && !pinned ? "true" : "false", pipeline ? "true" : "false",
          async_threads, naive_wave, upload_ms, register_s, sum.waves, sum.widest_wave, sum.gpu_waves,
          sum.cpu_waves, sum.split_waves, total, sum.gather_s, sum.hash_s, sum.upload_s, sum.wait_s);

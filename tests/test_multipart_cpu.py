@@ -116,3 +116,34 @@ def test_concurrent_files_under_tsan(mode):
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads(out.stdout)
     assert r["deadlock"] is False and all(m == gold[:12] for m in r["md5_files"])
+
+
+@pytest.mark.parametrize("fault,mode,want_uploaded", [
+    ("--short-read-part=9", [], None),
+    ("--short-read-part=9", ["--no-pipeline"], 8),
+    ("--short-read-part=1", [], 0),
+    ("--fail-upload-part=7", [], 6),
+    ("--fail-upload-part=7", ["--async=2"], 6),
+    ("--short-read-part=20", ["--async=3"], None),
+])
+def test_failures_stop_the_upload_and_return_every_buffer(fault, mode, want_uploaded):
+    """A short read (File::ReadNoLoad found a hole) or a failed upload stops
+    the file's upload, as the reference does (QSTransferManager.cpp:611-643):
+    no part at or after the failing one is handed on, the parts before the
+    failing wave keep their golden digests, and every buffer -- the wave's,
+    the one in upload, the one the helper thread was preparing -- is back in
+    the shared pool afterwards (pool_free_after == pool)."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    args = ["--aligned", "--size=%d" % (20 * 10 * MiB), "--pool=4", "--upload-ms=1", fault] + mode
+    out = run_raw(args, "cpu", timeout=120)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads(out.stdout)
+    bad = int(fault.split("=")[1])
+    assert r["error"], r
+    assert r["pool_free_after"] == 4, r
+    done = [i for i, h in enumerate(r["md5"]) if h]
+    assert all(i < bad - 1 for i in done), done           # nothing at or after the failing part
+    assert done == list(range(len(done)))                 # a prefix of the file, in order
+    assert [r["md5"][i] for i in done] == gold[:len(done)]
+    if want_uploaded is not None:
+        assert r["uploaded"] == want_uploaded, r
