@@ -137,6 +137,18 @@ print("child_ok=%s parent_ok=%s" % (child_ok, parent_ok))
 sys.exit(0 if child_ok and parent_ok else 1)
 '''
 
+LOG_SINK_GPU_SCRIPT = r'''
+import ctypes, sys
+import qsmd5
+got = []
+qsmd5.set_log_callback(lambda level, msg: got.append((level, msg)))
+bufs = [(ctypes.c_uint8 * (1 << 20))() for _ in range(64)]
+qsmd5.hash_batch([(ctypes.addressof(b), 1 << 20) for b in bufs], flags=qsmd5.FLAG_GPU_ONLY)
+qsmd5.hash_batch([b"abc"], flags=qsmd5.FLAG_CPU_ONLY)
+for level, msg in got:
+    print("%d|%s" % (level, msg))
+'''
+
 WORKER_SCRIPT = r'''
 import sys, ctypes
 import qsmd5
@@ -207,6 +219,23 @@ def test_fork_after_shutdown_child_makes_no_hip_call():
                          text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "child_ok=True parent_ok=True" in out.stdout
+
+
+@pytest.mark.cpu_backend
+def test_log_callback_names_the_bound_gpu_and_backends():
+    """qsmd5_set_log_callback on the MI355X: the GPU bound
+    at initialisation (gfx950, its CU count) and each call's backend, reason,
+    chunk count and bytes reach the host's logger at LogLevel Info, and
+    nothing of it reaches stderr."""
+    env = dict(ENV, QSMD5_BACKEND="auto")
+    out = subprocess.run([PY, "-c", LOG_SINK_GPU_SCRIPT], env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    lines = [ln.split("|", 1) for ln in out.stdout.splitlines() if "|" in ln]
+    assert any(lvl == "0" and m.startswith("qsmd5: bound GPU") and "gfx950" in m for lvl, m in lines), lines
+    assert ["0", "qsmd5: backend=gpu reason=forced chunks=64 bytes=67108864"] in lines, lines
+    assert ["0", "qsmd5: backend=cpu reason=forced chunks=1 bytes=3"] in lines, lines
+    assert "qsmd5:" not in out.stderr, out.stderr
 
 
 def test_concurrent_processes_one_gpu():
