@@ -193,6 +193,7 @@ struct Dev {
   HostPinned h_meta, h_dig;
   // Per-batch events, reused (batches on one Dev are serialised by mu).
   hipEvent_t ev_meta = nullptr, ev_first = nullptr, ev_last = nullptr;
+  hipEvent_t ev_done = nullptr;  // hipEventBlockingSync: the host sleeps on long batches
   uint64_t staging_cap = kDefaultStaging;
   double last_wall_ms = 0, last_kernel_ms = 0;
   std::atomic<uint32_t> chain_samples{0};  // batches that qualified as a chain-rate sample
@@ -279,7 +280,9 @@ int init_dev(Dev& d, int device) {
   d.staging_cap = env_u64("QSMD5_STAGING_BYTES", kDefaultStaging);
   if ((e = hipEventCreateWithFlags(&d.ev_meta, hipEventDisableTiming)) != hipSuccess ||
       (e = hipEventCreateWithFlags(&d.ev_first, hipEventDefault)) != hipSuccess ||
-      (e = hipEventCreateWithFlags(&d.ev_last, hipEventDefault)) != hipSuccess)
+      (e = hipEventCreateWithFlags(&d.ev_last, hipEventDefault)) != hipSuccess ||
+      (e = hipEventCreateWithFlags(&d.ev_done, hipEventBlockingSync | hipEventDisableTiming)) !=
+          hipSuccess)
     return hip_fail(e, "hipEventCreate");
   if ((e = qsmd5::warm_up(d.compute[0])) != hipSuccess ||
       (e = hipStreamSynchronize(d.compute[0])) != hipSuccess)
@@ -312,7 +315,7 @@ int release_dev(Dev& d) {
       chk(hipStreamDestroy(s));
       s = nullptr;
     }
-  for (hipEvent_t* e : {&d.ev_meta, &d.ev_first, &d.ev_last})
+  for (hipEvent_t* e : {&d.ev_meta, &d.ev_first, &d.ev_last, &d.ev_done})
     if (*e) {
       chk(hipEventDestroy(*e));
       *e = nullptr;
@@ -703,6 +706,43 @@ void note_gpu_chain(std::atomic<uint32_t>& dev_samples, uint64_t longest, size_t
   } while (!g_gpu_chain_bits.compare_exchange_weak(old, bits, std::memory_order_relaxed));
 }
 
+double gpu_est_ms(uint64_t longest, uint64_t host_bytes);  // routing cost model, below
+
+// How the calling thread waits for a synchronous batch.  hipStreamSynchronize
+// spins a host core for the whole batch; a GPU batch of 10 MiB parts is one
+// ~85 ms chain, and the route sweep measured ~2 host cores busy per GPU wave
+// that way (profiles/r04_route_sweep.jsonl: 5.5 CPU-s for 32 eight-part
+// waves), which defeats the point of leaving qsfs's cores to qsfs.  So a
+// batch the cost model expects to take >= 1 ms waits on an event created
+// with hipEventBlockingSync (the thread sleeps until the GPU signals);
+// shorter ones keep the spin, whose wake-up is faster than a blocked
+// thread's.  QSMD5_WAIT=spin / block forces one or the other.
+int wait_mode() {  // 0 auto, 1 block, 2 spin, 3 poll
+  static const int mode = [] {
+    const char* e = getenv("QSMD5_WAIT");
+    return !e || !*e || !strcmp(e, "auto") ? 0 : !strcmp(e, "block") ? 1 : !strcmp(e, "poll") ? 3 : 2;
+  }();
+  return mode;
+}
+
+// Wait for everything enqueued on stream s of GPU d (caller holds d.mu).
+hipError_t wait_stream(Dev& d, hipStream_t s, double est_ms) {
+  const int mode = wait_mode();
+  if (mode == 2 || (mode == 0 && est_ms < 1.0)) return hipStreamSynchronize(s);
+  hipError_t e = hipEventRecord(d.ev_done, s);
+  if (e != hipSuccess) return e;
+  if (mode == 1) return hipEventSynchronize(d.ev_done);
+  // poll: sleep through most of the expected time, then check every 100 us
+  auto t0 = std::chrono::steady_clock::now();
+  std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(est_ms * 900.0)));
+  for (;;) {
+    e = hipEventQuery(d.ev_done);
+    if (e != hipErrorNotReady) return e;
+    std::this_thread::sleep_for(std::chrono::microseconds(
+        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2) ? 1000 : 100));
+  }
+}
+
 // The synchronous batch on one GPU: device chunks in one launch; host chunks
 // staged in slices with copy/compute overlap.  Caller holds r.mu and has made
 // r.device current.  Device chunks must live on r.device: a kernel reading
@@ -1062,8 +1102,11 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   }
   if (!first_kernel) QS_HIP(hipEventRecord(r.ev_last, s0));
   QS_HIP(hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0));
-  hipError_t e = hipStreamSynchronize(s0);
-  if (e != hipSuccess) return drain(hip_fail(e, "hipStreamSynchronize"));
+  uint64_t longest_len = 0, host_bytes = 0;
+  for (size_t i = 0; i < n; ++i) longest_len = std::max(longest_len, len[i]);
+  for (uint64_t L : host_len) host_bytes += L;
+  hipError_t e = wait_stream(r, s0, gpu_est_ms(longest_len, host_bytes));
+  if (e != hipSuccess) return drain(hip_fail(e, "waiting for the batch"));
   memcpy(digests, r.h_dig.p, n * 16);
   if (trace) {
     auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
@@ -2505,7 +2548,7 @@ static int ctx_blocks(qsmd5_ctx* c, const uint8_t* p, uint64_t nblk, bool on_dev
     QS_HIP(qsmd5::launch_column(c->d_seg, reinterpret_cast<const uint32_t*>(c->d_seg + 16), 1,
                                 reinterpret_cast<uint32_t*>(c->d_seg + 32), c->hashed, step * 64,
                                 c->d_state, s));
-    QS_HIP(hipStreamSynchronize(s));  // seg lives on this stack frame
+    QS_HIP(wait_stream(r, s, gpu_est_ms(step * 64, on_device ? 0 : step * 64)));  // seg lives on this frame
     src += step * 64;
     c->hashed += step * 64;
     nblk -= step;

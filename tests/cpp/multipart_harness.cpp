@@ -32,6 +32,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <dirent.h>
+#include <pthread.h>
 #include <sys/resource.h>
 #include <unistd.h>
 
@@ -160,7 +162,11 @@ class WatchedPool {
 class Executor {
  public:
   explicit Executor(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
+    for (int i = 0; i < n; ++i)
+      th_.emplace_back([this] {
+        pthread_setname_np(pthread_self(), "executor");
+        loop();
+      });
   }
   ~Executor() {
     {
@@ -226,6 +232,39 @@ double cpu_seconds() {
   struct rusage ru;
   getrusage(RUSAGE_SELF, &ru);
   return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
+}
+
+// Busy threads of this process so far: "name:cpu_s" for each thread that
+// used more than 50 ms (/proc/self/task/*/stat utime + stime), to see which
+// thread a backend keeps busy (the runtime's caller, HIP's own threads).
+std::string busy_threads() {
+  std::string out;
+  const long hz = sysconf(_SC_CLK_TCK);
+  DIR* dir = opendir("/proc/self/task");
+  if (!dir) return out;
+  while (struct dirent* de = readdir(dir)) {
+    if (de->d_name[0] < '0' || de->d_name[0] > '9') continue;
+    const std::string path = std::string("/proc/self/task/") + de->d_name + "/stat";
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) continue;
+    char buf[1024];
+    const size_t got = fread(buf, 1, sizeof(buf) - 1, f);
+    fclose(f);
+    buf[got] = 0;
+    const char* l = strchr(buf, '(');
+    const char* r = strrchr(buf, ')');
+    if (!l || !r) continue;
+    const std::string comm(l + 1, r);
+    unsigned long ut = 0, st = 0;
+    // after ") ": state ppid pgrp session tty tpgid flags minflt cminflt majflt cmajflt utime stime
+    if (sscanf(r + 2, "%*c %*d %*d %*d %*d %*d %*u %*u %*u %*u %*u %lu %lu", &ut, &st) != 2) continue;
+    const double cs = (double)(ut + st) / hz;
+    if (cs < 0.05) continue;
+    out += std::string(out.empty() ? "" : ", ") + "\"" + comm + ":" + de->d_name + "\": " +
+           std::to_string(cs);
+  }
+  closedir(dir);
+  return out;
 }
 
 void sleep_ms(double ms) {
@@ -364,6 +403,7 @@ int main(int argc, char** argv) {
   std::atomic<bool> finished{false};
   progress();
   std::thread watchdog([&] {
+    pthread_setname_np(pthread_self(), "watchdog");
     while (!finished.load()) {
       std::this_thread::sleep_for(std::chrono::milliseconds(50));
       const double idle = (clock_type::now().time_since_epoch().count() - g_progress_ns.load()) * 1e-9;
@@ -390,6 +430,7 @@ int main(int argc, char** argv) {
     std::vector<std::thread> th;
     for (size_t f = 0; f < files; ++f) {
       th.emplace_back([&, f] {
+        pthread_setname_np(pthread_self(), ("flush-" + std::to_string(f)).c_str());
         const PagedFile& pf = file[aligned ? 0 : f];
         try {
           if (naive_wave) {
@@ -490,7 +531,7 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < hash_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", hash_runs[i]);
   printf("], \"wall_s_runs\": [");
   for (size_t i = 0; i < wall_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", wall_runs[i]);
-  printf("], \"cpu_s_runs\": [");
+  printf("], \"busy_threads\": {%s}, \"cpu_s_runs\": [", busy_threads().c_str());
   for (size_t i = 0; i < cpu_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", cpu_runs[i]);
   printf("], \"md5\": %s, \"md5_files\": [", md5_list(md5[0]).c_str());
   for (size_t f = 0; f < files; ++f) printf("%s%s", f ? ", " : "", md5_list(md5[f]).c_str());
