@@ -709,14 +709,17 @@ void note_gpu_chain(std::atomic<uint32_t>& dev_samples, uint64_t longest, size_t
 double gpu_est_ms(uint64_t longest, uint64_t host_bytes);  // routing cost model, below
 
 // How the calling thread waits for a synchronous batch.  hipStreamSynchronize
-// spins a host core for the whole batch; a GPU batch of 10 MiB parts is one
-// ~85 ms chain, and the route sweep measured ~2 host cores busy per GPU wave
-// that way (profiles/r04_route_sweep.jsonl: 5.5 CPU-s for 32 eight-part
-// waves), which defeats the point of leaving qsfs's cores to qsfs.  So a
-// batch the cost model expects to take >= 1 ms waits on an event created
-// with hipEventBlockingSync (the thread sleeps until the GPU signals);
-// shorter ones keep the spin, whose wake-up is faster than a blocked
-// thread's.  QSMD5_WAIT=spin / block forces one or the other.
+// spins a host core for the whole batch, and so does hipEventSynchronize even
+// on a hipEventBlockingSync event (ubench/thread_cpu_probe.hip: 80 ms waits
+// cost the caller 80 ms of CPU in all three forms).  A GPU batch of 10 MiB
+// parts is one ~85 ms chain, so a daemon that sends waves to the GPU to keep
+// its cores for itself would lose one core per waiting thread.  A batch the
+// cost model expects to take >= 1 ms therefore sleeps through 90% of that
+// estimate and then checks an event every 100 us (QSMD5_WAIT=poll; the
+// route sweep's 32 GPU waves of 8 parts: the caller's CPU went from 2.7 s to
+// ~0, same wall time, profiles/r04_wait_ab.log); shorter batches keep the
+// spin, which wakes faster (a 1 KiB call stays at ~39 us).
+// QSMD5_WAIT=spin / block / poll forces one form for every batch.
 int wait_mode() {  // 0 auto, 1 block, 2 spin, 3 poll
   static const int mode = [] {
     const char* e = getenv("QSMD5_WAIT");
@@ -733,8 +736,9 @@ hipError_t wait_stream(Dev& d, hipStream_t s, double est_ms) {
   if (e != hipSuccess) return e;
   if (mode == 1) return hipEventSynchronize(d.ev_done);
   // poll: sleep through most of the expected time, then check every 100 us
+  // (every 1 ms once a batch runs 2 s past its start: a shared or slow GPU)
   auto t0 = std::chrono::steady_clock::now();
-  std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(est_ms * 900.0)));
+  if (est_ms > 0) std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(est_ms * 900.0)));
   for (;;) {
     e = hipEventQuery(d.ev_done);
     if (e != hipErrorNotReady) return e;
