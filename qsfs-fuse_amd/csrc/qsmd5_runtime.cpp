@@ -728,6 +728,25 @@ int wait_mode() {  // 0 auto, 1 block, 2 spin, 3 poll
   return mode;
 }
 
+// Wait for event ev, expected in about est_ms: spin below 1 ms, otherwise
+// sleep through 90% of it and poll (see wait_mode; QSMD5_WAIT=spin/block
+// force the HIP waits).
+hipError_t wait_event(hipEvent_t ev, double est_ms) {
+  const int mode = wait_mode();
+  if (mode == 2 || mode == 1 || (mode == 0 && est_ms < 1.0)) {
+    const hipError_t q = hipEventQuery(ev);  // often done already: no HIP wait at all
+    return q == hipErrorNotReady ? hipEventSynchronize(ev) : q;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(est_ms * 900.0)));
+  for (;;) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e != hipErrorNotReady) return e;
+    std::this_thread::sleep_for(std::chrono::microseconds(
+        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2) ? 1000 : 100));
+  }
+}
+
 // Wait for everything enqueued on stream s of GPU d (caller holds d.mu).
 hipError_t wait_stream(Dev& d, hipStream_t s, double est_ms) {
   const int mode = wait_mode();
@@ -961,7 +980,6 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   // events); several slices overlap copies and kernels over the streams.
   const bool one_stream = slices.size() <= 1;
   if (!one_stream) QS_HIP(hipEventRecord(r.ev_meta, s0));
-  std::vector<hipEvent_t> region_free(nregions, nullptr);
   // QSMD5_TRACE=1: per-slice copy/kernel timeline on stderr (diagnostics).
   const bool trace = env_u64("QSMD5_TRACE", 0) != 0;
   std::vector<hipEvent_t> tr(trace ? 4 * slices.size() + 1 : 0, nullptr);
@@ -974,7 +992,6 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   uint32_t* d_dig = static_cast<uint32_t*>(r.d_dig.p);
   bool first_kernel = true;
   unsigned launches = 0;   // hashing launches (a chain-rate sample needs exactly one)
-  size_t gather_next = 0;  // gather rows launched so far (slices take them in order)
   unsigned used = 0;  // compute streams (1..) that ran work: joined into s0 at the end
   auto mark_first = [&](hipStream_t s) -> int {
     if (first_kernel) {
@@ -1007,23 +1024,37 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   // compute stream (so a group's columns run in order) once the copy and the
   // descriptors have landed.  Runs of equal-length chunks at a constant host
   // stride inside one allocation (a file's parts) go as one 2-D copy per column.
-  for (size_t si = 0; si < slices.size(); ++si) {
+  //
+  // The order between copy and compute streams is kept by THIS thread, not by
+  // hipStreamWaitEvent: while a stream holds a wait on another stream's
+  // pending event, HIP keeps one of its own threads polling for the whole
+  // batch -- a host core per batch (ubench/thread_cpu_probe.hip: 40 column
+  // slices ordered by stream waits, 0.91 cores; the same slices ordered by the
+  // host, 0; equal wall time).  So a slice's copies are enqueued once the host
+  // has seen the kernel that last used its region finish, and its kernel is
+  // launched once the host has seen its copies land; the thread sleeps between
+  // checks (20 us, backing off to 200 us while nothing moves).  Copies run
+  // nregions slices ahead and kernels queue behind each other, so neither
+  // engine idles on the host's latency.  A single slice needs no ordering: its
+  // copy and kernel run on s0 in stream order.
+  const size_t S = slices.size();
+  std::vector<hipEvent_t> copied(one_stream ? 0 : S, nullptr), done(one_stream ? 0 : S, nullptr);
+  std::vector<size_t> gather_first(S + 1, 0);  // gather rows of slice si: [first[si], first[si + 1])
+  for (size_t si = 0; si < S; ++si) {
+    size_t k = 0;
+    if (!inline_data)
+      for (const qsmd5::CopyRun& run : slice_runs[si]) k += gathered(slices[si], run) ? 1 : 0;
+    gather_first[si + 1] = gather_first[si] + k;
+  }
+  auto slice_gathers = [&](size_t si) { return gather_first[si + 1] - gather_first[si]; };
+  // The slice's copies (planned above): 2-D runs and single rows by DMA,
+  // gathered rows by one kernel launch; then `copied[si]` on the copy stream.
+  auto enqueue_copies = [&](size_t si, hipStream_t cp) -> int {
     const qsmd5::Slice& sl = slices[si];
     const qsmd5::Group& g = groups[sl.group];
-    const size_t reg = si % nregions;
-    const int csi = one_stream ? 0 : 1 + (int)(sl.group % (kComputeStreams - 1));
-    hipStream_t cs = r.compute[csi];
-    hipStream_t cp = one_stream ? s0 : r.copy[si % r.ncopy];
-    used |= 1u << csi;
-    if (region_free[reg]) {
-      hipError_t e = hipStreamWaitEvent(cp, region_free[reg], 0);
-      if (e != hipSuccess) return drain(hip_fail(e, "hipStreamWaitEvent"));
-    }
     const uint64_t col_off = W == kNoColumns ? 0 : (uint64_t)sl.col * W;
     uint8_t* dst = slice_base[si];
     if (trace) QS_HIP(hipEventRecord(tr[4 * si], cp));
-    // The slice's copies (planned above): 2-D runs and single rows by DMA,
-    // gathered rows by one kernel launch.
     size_t slice_gather = 0;
     static const std::vector<qsmd5::CopyRun> kNoRuns;  // inline data: already in the meta copy
     const std::vector<qsmd5::CopyRun>& runs = inline_data ? kNoRuns : slice_runs[si];
@@ -1052,64 +1083,128 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       } else {
         e = hipMemcpyAsync(dst, src, w, hipMemcpyHostToDevice, cp);
       }
-      if (e != hipSuccess) return drain(hip_fail(e, "hipMemcpyAsync H2D"));
+      if (e != hipSuccess) return hip_fail(e, "hipMemcpyAsync H2D");
       dst += run.rows * stage_bytes(w);
     }
-    if (slice_gather) {
-      // the gather rows live in the metadata block copied on s0
-      hipError_t e = one_stream ? hipSuccess : hipStreamWaitEvent(cp, r.ev_meta, 0);
-      if (e == hipSuccess)
-        e = qsmd5::launch_gather(dm + gather_off + gather_next * qsmd5::kGatherRowBytes,
-                                 (uint32_t)slice_gather, cp,
-                                 (uint32_t)env_u64("QSMD5_GATHER_GROUPS", 8));
-      if (e != hipSuccess) return drain(hip_fail(e, "qsmd5 gather launch"));
-      gather_next += slice_gather;
+    if (slice_gather) {  // the gather rows live in the metadata block (landed: see below)
+      hipError_t e = qsmd5::launch_gather(dm + gather_off + gather_first[si] * qsmd5::kGatherRowBytes,
+                                          (uint32_t)slice_gather, cp,
+                                          (uint32_t)env_u64("QSMD5_GATHER_GROUPS", 8));
+      if (e != hipSuccess) return hip_fail(e, "qsmd5 gather launch");
     }
     if (trace) QS_HIP(hipEventRecord(tr[4 * si + 1], cp));
-    hipError_t e = hipSuccess;
     if (!one_stream) {
-      hipEvent_t copied = nullptr;
-      if (int rc = events.make(&copied, hipEventDisableTiming)) return drain(rc);
-      e = hipEventRecord(copied, cp);
-      if (e == hipSuccess) e = hipStreamWaitEvent(cs, copied, 0);
-      if (e == hipSuccess) e = hipStreamWaitEvent(cs, r.ev_meta, 0);
-      if (e != hipSuccess) return drain(hip_fail(e, "stream ordering"));
+      if (int rc = events.make(&copied[si], hipEventDisableTiming)) return rc;
+      QS_HIP(hipEventRecord(copied[si], cp));
     }
+    return 0;
+  };
+  // The slice's kernel on its compute stream; then `done[si]` if a later
+  // slice reuses the region.
+  auto launch_slice = [&](size_t si, hipStream_t cs) -> int {
+    const qsmd5::Slice& sl = slices[si];
+    const qsmd5::Group& g = groups[sl.group];
+    const uint64_t col_off = W == kNoColumns ? 0 : (uint64_t)sl.col * W;
     if (trace) QS_HIP(hipEventRecord(tr[4 * si + 2], cs));
     if (g.ncols > 1) {
-      if (int rc = mark_first(cs)) return drain(rc);
+      if (int rc = mark_first(cs)) return rc;
       ++launches;
-      e = qsmd5::launch_column(d_seg + sl.seg0, d_order + n + sl.seg0, (uint32_t)sl.active, d_dig,
-                               col_off, W, static_cast<uint32_t*>(r.d_state.p), cs);
-      if (e != hipSuccess) return drain(hip_fail(e, "qsmd5 column kernel launch"));
+      hipError_t e = qsmd5::launch_column(d_seg + sl.seg0, d_order + n + sl.seg0, (uint32_t)sl.active,
+                                          d_dig, col_off, W, static_cast<uint32_t*>(r.d_state.p), cs);
+      if (e != hipSuccess) return hip_fail(e, "qsmd5 column kernel launch");
     } else {
       // staged chunks sit at 256-B-aligned offsets plus a 16-B-multiple skew
-      if (int rc = launch(cs, d_order + dev_idx.size() + g.first, sl.active, true, 0))
-        return drain(rc);
+      if (int rc = launch(cs, d_order + dev_idx.size() + g.first, sl.active, true, 0)) return rc;
     }
-    if (!one_stream && nregions < slices.size()) {  // a later slice reuses this region
-      hipEvent_t done = nullptr;
-      if (int rc = events.make(&done, hipEventDisableTiming)) return drain(rc);
-      if ((e = hipEventRecord(done, cs)) != hipSuccess) return drain(hip_fail(e, "hipEventRecord"));
-      region_free[reg] = done;
+    if (!one_stream && si + nregions < S) {  // a later slice reuses this region
+      if (int rc = events.make(&done[si], hipEventDisableTiming)) return rc;
+      QS_HIP(hipEventRecord(done[si], cs));
     }
     if (trace) QS_HIP(hipEventRecord(tr[4 * si + 3], cs));
+    return 0;
+  };
+  auto compute_stream_of = [&](size_t si) {
+    return one_stream ? 0 : 1 + (int)(slices[si].group % (kComputeStreams - 1));
+  };
+  // 1 = complete, 0 = pending, -1 = error (t_last_error set)
+  auto landed = [&](hipEvent_t ev) -> int {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 1;
+    if (q == hipErrorNotReady) return 0;
+    (void)hip_fail(q, "waiting for a staging step");
+    return -1;
+  };
+  if (one_stream) {
+    if (S) {
+      used |= 1u;
+      if (int rc = enqueue_copies(0, s0)) return drain(rc);
+      if (int rc = launch_slice(0, s0)) return drain(rc);
+    }
+  } else {
+    size_t nc = 0, nk = 0;  // slices whose copies / kernels are enqueued
+    bool meta = false;      // the metadata block (descriptors, gather rows) has landed
+    int idle_us = 20;
+    while (nk < S) {
+      bool moved = false;
+      if (!meta) {
+        const int q = landed(r.ev_meta);
+        if (q < 0) return drain(-EIO);
+        meta = q == 1;
+      }
+      while (nc < S) {
+        if (nc >= nregions) {  // its region: free once the host saw the last user's kernel end
+          if (nc - nregions >= nk) break;  // that kernel is not even launched yet
+          const int q = landed(done[nc - nregions]);
+          if (q < 0) return drain(-EIO);
+          if (!q) break;
+        }
+        if (slice_gathers(nc) && !meta) break;  // the gather kernel reads rows from the meta block
+        if (int rc = enqueue_copies(nc, r.copy[nc % r.ncopy])) return drain(rc);
+        ++nc;
+        moved = true;
+      }
+      while (nk < nc && meta) {
+        const int q = landed(copied[nk]);
+        if (q < 0) return drain(-EIO);
+        if (!q) break;
+        const int csi = compute_stream_of(nk);
+        used |= 1u << csi;
+        if (int rc = launch_slice(nk, r.compute[csi])) return drain(rc);
+        ++nk;
+        moved = true;
+      }
+      if (nk == S) break;
+      if (moved) {
+        idle_us = 20;
+      } else {
+        std::this_thread::sleep_for(std::chrono::microseconds(idle_us));
+        idle_us = std::min(200, idle_us * 2);
+      }
+    }
   }
-  // Join the compute streams that ran work into s0, then fetch the digests.
+  // Every kernel is enqueued.  The compute streams that ran slices end with a
+  // timing event each; the host sees them all complete before the digests
+  // come back on s0 (after s0's own device-chunk kernel, in stream order).
+  std::vector<hipEvent_t> tails;
   for (int k = 1; k < kComputeStreams; ++k) {
     if (!(used & (1u << k))) continue;
-    hipEvent_t j = nullptr;
-    if (int rc = events.make(&j, hipEventDisableTiming)) return drain(rc);
-    hipError_t e = hipEventRecord(j, r.compute[k]);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s0, j, 0);
-    if (e != hipSuccess) return drain(hip_fail(e, "stream join"));
+    hipEvent_t t = nullptr;
+    if (int rc = events.make(&t, hipEventDefault)) return drain(rc);
+    QS_HIP(hipEventRecord(t, r.compute[k]));
+    tails.push_back(t);
   }
   if (!first_kernel) QS_HIP(hipEventRecord(r.ev_last, s0));
-  QS_HIP(hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0));
   uint64_t longest_len = 0, host_bytes = 0;
   for (size_t i = 0; i < n; ++i) longest_len = std::max(longest_len, len[i]);
   for (uint64_t L : host_len) host_bytes += L;
-  hipError_t e = wait_stream(r, s0, gpu_est_ms(longest_len, host_bytes));
+  const double est_ms = gpu_est_ms(longest_len, host_bytes);
+  const double spent_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_planned).count();
+  for (hipEvent_t t : tails) {
+    const hipError_t e = wait_event(t, est_ms - spent_ms);
+    if (e != hipSuccess) return drain(hip_fail(e, "waiting for the batch"));
+  }
+  QS_HIP(hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0));
+  hipError_t e = wait_stream(r, s0, tails.empty() ? est_ms - spent_ms : 0.0);
   if (e != hipSuccess) return drain(hip_fail(e, "waiting for the batch"));
   memcpy(digests, r.h_dig.p, n * 16);
   if (trace) {
@@ -1135,6 +1230,9 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   float kms = 0;
   r.last_kernel_ms =
       (!first_kernel && hipEventElapsedTime(&kms, r.ev_first, r.ev_last) == hipSuccess) ? kms : 0.0;
+  for (hipEvent_t t : tails)  // slices on the other compute streams
+    if (!first_kernel && hipEventElapsedTime(&kms, r.ev_first, t) == hipSuccess)
+      r.last_kernel_ms = std::max(r.last_kernel_ms, (double)kms);
   {
     uint64_t longest = 0;
     for (uint64_t L : len) longest = std::max(longest, L);

@@ -30,6 +30,7 @@
 #include <map>
 #include <string>
 #include <thread>
+#include <vector>
 
 #define CHECK(x)                                                                \
   do {                                                                          \
@@ -113,10 +114,20 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreateWithFlags(&ev_t0, hipEventDefault));
   CHECK(hipEventCreateWithFlags(&ev_t1, hipEventDefault));
   const char* modes[] = {"stream", "event", "blocking", "poll", "copy1d", "copy2d", "samestream",
-                         "timing", "d2h_pinned", "d2h_spin"};
+                         "timing", "d2h_pinned", "d2h_spin", "pipe40", "pipe40_1s", "pipe40_noev",
+                         "pipe40_host"};
+  // modes 10-12: the runtime's column pipeline -- 40 slices, each a 2-D copy
+  // of 8 rows x 256 KiB on a copy stream, an event, the compute stream
+  // waiting on it, and a kernel of 1/40 of the wave -- then the poll wait;
+  // pipe40_1s puts copies and kernels on one stream (no events);
+  // pipe40_noev keeps two streams but orders them with one event at the end;
+  // pipe40_host orders them on the host: kernel k is launched once the host
+  // sees copy k's event complete (hipEventQuery, 50 us sleeps), no stream waits.
+  std::vector<hipEvent_t> evs(40);
+  for (auto& e : evs) CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   uint8_t* hsmall = nullptr;  // modes 8-9: the digests' D2H copy into pinned memory after the kernel
   CHECK(hipHostMalloc(reinterpret_cast<void**>(&hsmall), 1 << 16, hipHostMallocDefault));
-  for (int m = 0; m < 10; ++m) {
+  for (int m = 0; m < 14; ++m) {
     const auto before = threads_cpu();
     const auto t0 = std::chrono::steady_clock::now();
     for (int r = 0; r < reps; ++r) {
@@ -128,10 +139,39 @@ int main(int argc, char** argv) {
       } else if (m == 6) {
         CHECK(hipMemcpyAsync(dbuf, h, rows * row, hipMemcpyHostToDevice, s));
       }
+      if (m == 13) {
+        for (int k = 0; k < 40; ++k) {
+          CHECK(hipMemcpy2DAsync(dbuf + (size_t)k * (256 << 10), row + 4096, (uint8_t*)h + (size_t)k * (256 << 10),
+                                 row, 256 << 10, rows, hipMemcpyHostToDevice, s2));
+          CHECK(hipEventRecord(evs[k], s2));
+        }
+        for (int k = 0; k < 40; ++k) {
+          while (hipEventQuery(evs[k]) == hipErrorNotReady)
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+          hipLaunchKernelGGL(hold, dim3(8), dim3(64), 0, s, ticks / 40, d);
+        }
+      } else if (m >= 10) {
+        for (int k = 0; k < 40; ++k) {
+          hipStream_t cs = m == 11 ? s : s2;
+          CHECK(hipMemcpy2DAsync(dbuf + (size_t)k * (256 << 10), row + 4096, (uint8_t*)h + (size_t)k * (256 << 10),
+                                 row, 256 << 10, rows, hipMemcpyHostToDevice, cs));
+          if (m == 10) {
+            CHECK(hipEventRecord(evs[k], s2));
+            CHECK(hipStreamWaitEvent(s, evs[k], 0));
+          }
+          if (m != 12) hipLaunchKernelGGL(hold, dim3(8), dim3(64), 0, s, ticks / 40, d);
+        }
+        if (m == 12) {
+          CHECK(hipEventRecord(evs[0], s2));
+          CHECK(hipStreamWaitEvent(s, evs[0], 0));
+          for (int k = 0; k < 40; ++k) hipLaunchKernelGGL(hold, dim3(8), dim3(64), 0, s, ticks / 40, d);
+        }
+      } else {
       if (m == 7) CHECK(hipEventRecord(ev_t0, s));
       hipLaunchKernelGGL(hold, dim3(8), dim3(64), 0, s, ticks, d);
       if (m == 7) CHECK(hipEventRecord(ev_t1, s));
       if (m >= 8) CHECK(hipMemcpyAsync(hsmall, d, 4096, hipMemcpyDeviceToHost, s));
+      }
       if (m == 9) {
         CHECK(hipStreamSynchronize(s));
       } else if (m >= 4) {
