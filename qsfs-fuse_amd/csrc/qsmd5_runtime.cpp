@@ -728,25 +728,6 @@ int wait_mode() {  // 0 auto, 1 block, 2 spin, 3 poll
   return mode;
 }
 
-// Wait for event ev, expected in about est_ms: spin below 1 ms, otherwise
-// sleep through 90% of it and poll (see wait_mode; QSMD5_WAIT=spin/block
-// force the HIP waits).
-hipError_t wait_event(hipEvent_t ev, double est_ms) {
-  const int mode = wait_mode();
-  if (mode == 2 || mode == 1 || (mode == 0 && est_ms < 1.0)) {
-    const hipError_t q = hipEventQuery(ev);  // often done already: no HIP wait at all
-    return q == hipErrorNotReady ? hipEventSynchronize(ev) : q;
-  }
-  const auto t0 = std::chrono::steady_clock::now();
-  std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(est_ms * 900.0)));
-  for (;;) {
-    const hipError_t e = hipEventQuery(ev);
-    if (e != hipErrorNotReady) return e;
-    std::this_thread::sleep_for(std::chrono::microseconds(
-        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2) ? 1000 : 100));
-  }
-}
-
 // Wait for everything enqueued on stream s of GPU d (caller holds d.mu).
 hipError_t wait_stream(Dev& d, hipStream_t s, double est_ms) {
   const int mode = wait_mode();
@@ -1197,14 +1178,24 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   uint64_t longest_len = 0, host_bytes = 0;
   for (size_t i = 0; i < n; ++i) longest_len = std::max(longest_len, len[i]);
   for (uint64_t L : host_len) host_bytes += L;
-  const double est_ms = gpu_est_ms(longest_len, host_bytes);
-  const double spent_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_planned).count();
+  // The compute streams' queued kernels: how much is left is not known here
+  // (a group's columns run one after another behind its copies), so the host
+  // keeps polling, backing off from 20 us to 500 us.
   for (hipEvent_t t : tails) {
-    const hipError_t e = wait_event(t, est_ms - spent_ms);
-    if (e != hipSuccess) return drain(hip_fail(e, "waiting for the batch"));
+    int idle_us = 20;
+    for (;;) {
+      const int q = landed(t);
+      if (q < 0) return drain(-EIO);
+      if (q) break;
+      std::this_thread::sleep_for(std::chrono::microseconds(idle_us));
+      idle_us = std::min(500, idle_us * 2);
+    }
   }
   QS_HIP(hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0));
-  hipError_t e = wait_stream(r, s0, tails.empty() ? est_ms - spent_ms : 0.0);
+  // one stream (a single slice, or device chunks only): copy and kernel in
+  // stream order, so the cost model's copy + chain is what is left to wait
+  const double est_ms = tails.empty() ? gpu_est_ms(longest_len, host_bytes) : 0.0;
+  hipError_t e = wait_stream(r, s0, est_ms);
   if (e != hipSuccess) return drain(hip_fail(e, "waiting for the batch"));
   memcpy(digests, r.h_dig.p, n * 16);
   if (trace) {
