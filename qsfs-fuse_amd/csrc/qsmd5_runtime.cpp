@@ -1132,7 +1132,12 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
         if (q < 0) return drain(-EIO);
         meta = q == 1;
       }
-      while (nc < S) {
+      // one slice's copies per turn, then whatever kernels are ready: a
+      // pageable source makes HIP stage the copy on this thread before the
+      // call returns, and the kernels of the slices before it must not wait
+      // for all of that
+      do {
+        if (nc >= S) break;
         if (nc >= nregions) {  // its region: free once the host saw the last user's kernel end
           if (nc - nregions >= nk) break;  // that kernel is not even launched yet
           const int q = landed(done[nc - nregions]);
@@ -1143,7 +1148,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
         if (int rc = enqueue_copies(nc, r.copy[nc % r.ncopy])) return drain(rc);
         ++nc;
         moved = true;
-      }
+      } while (false);
       while (nk < nc && meta) {
         const int q = landed(copied[nk]);
         if (q < 0) return drain(-EIO);
