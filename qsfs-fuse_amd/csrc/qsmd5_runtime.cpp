@@ -706,7 +706,8 @@ void note_gpu_chain(std::atomic<uint32_t>& dev_samples, uint64_t longest, size_t
   } while (!g_gpu_chain_bits.compare_exchange_weak(old, bits, std::memory_order_relaxed));
 }
 
-double gpu_est_ms(uint64_t longest, uint64_t host_bytes);  // routing cost model, below
+double gpu_est_ms(uint64_t longest, uint64_t host_bytes);       // routing cost model, below
+double gpu_wait_est_ms(uint64_t longest, uint64_t host_bytes);  // its lower bound, for sleeping
 
 // How the calling thread waits for a synchronous batch.  hipStreamSynchronize
 // spins a host core for the whole batch, and so does hipEventSynchronize even
@@ -735,7 +736,8 @@ hipError_t wait_stream(Dev& d, hipStream_t s, double est_ms) {
   hipError_t e = hipEventRecord(d.ev_done, s);
   if (e != hipSuccess) return e;
   if (mode == 1) return hipEventSynchronize(d.ev_done);
-  // poll: sleep through most of the expected time, then check every 100 us
+  // poll: sleep through most of the expected time (est_ms is the batch's
+  // shortest plausible time, gpu_wait_est_ms), then check every 100 us
   // (every 1 ms once a batch runs 2 s past its start: a shared or slow GPU)
   auto t0 = std::chrono::steady_clock::now();
   if (est_ms > 0) std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(est_ms * 900.0)));
@@ -807,6 +809,8 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   int64_t column_bytes = -1;  // automatic
   if (const char* ev = getenv("QSMD5_COLUMN_BYTES"); ev && *ev)
     column_bytes = (int64_t)env_u64("QSMD5_COLUMN_BYTES", 0);  // 0 = whole chunks
+  // read per batch (tests shrink the ring to one region to drive region reuse)
+  r.staging_cap = env_u64("QSMD5_STAGING_BYTES", kDefaultStaging);
   const qsmd5::HostPlan plan =
       qsmd5::plan_host(host_len, r.staging_cap, env_u64("QSMD5_SLICE_BYTES", 0), column_bytes);
   const auto t_hostplan = std::chrono::steady_clock::now();
@@ -1199,7 +1203,7 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   QS_HIP(hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0));
   // one stream (a single slice, or device chunks only): copy and kernel in
   // stream order, so the cost model's copy + chain is what is left to wait
-  const double est_ms = tails.empty() ? gpu_est_ms(longest_len, host_bytes) : 0.0;
+  const double est_ms = tails.empty() ? gpu_wait_est_ms(longest_len, host_bytes) : 0.0;
   hipError_t e = wait_stream(r, s0, est_ms);
   if (e != hipSuccess) return drain(hip_fail(e, "waiting for the batch"));
   memcpy(digests, r.h_dig.p, n * 16);
@@ -1728,6 +1732,15 @@ double link_gibs() {
 // `total` bytes of which `d2h_bytes` must first be read back from a GPU.
 double gpu_est_ms(uint64_t longest, uint64_t host_bytes) {
   return kGpuCallMs + 1e3 * ((double)longest / gpu_chain_gibs() + (double)host_bytes / link_gibs()) / kGiB;
+}
+// The shortest time the same batch can plausibly take, for how long a waiting
+// thread may sleep before it starts polling (wait_stream): a measured chain
+// rate pulled down by a slow sample (a shared GPU) must not make the caller
+// oversleep, so the chain is priced at the faster of the measured and the
+// nominal rate.
+double gpu_wait_est_ms(uint64_t longest, uint64_t host_bytes) {
+  const double chain = std::max(gpu_chain_gibs(), kGpuChainGiBs);
+  return 1e3 * ((double)longest / chain + (double)host_bytes / link_gibs()) / kGiB;
 }
 double cpu_est_ms(uint64_t longest, uint64_t total, uint64_t d2h_bytes = 0) {
   const double T = (double)cpu_threads(), rc = cpu_gibs_per_thread();
@@ -2646,7 +2659,7 @@ static int ctx_blocks(qsmd5_ctx* c, const uint8_t* p, uint64_t nblk, bool on_dev
     QS_HIP(qsmd5::launch_column(c->d_seg, reinterpret_cast<const uint32_t*>(c->d_seg + 16), 1,
                                 reinterpret_cast<uint32_t*>(c->d_seg + 32), c->hashed, step * 64,
                                 c->d_state, s));
-    QS_HIP(wait_stream(r, s, gpu_est_ms(step * 64, on_device ? 0 : step * 64)));  // seg lives on this frame
+    QS_HIP(wait_stream(r, s, gpu_wait_est_ms(step * 64, on_device ? 0 : step * 64)));  // seg lives on this frame
     src += step * 64;
     c->hashed += step * 64;
     nblk -= step;

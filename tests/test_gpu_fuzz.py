@@ -10,7 +10,10 @@ duplicates, and the runtime's knobs drawn per batch:
 - QSMD5_GATHER / QSMD5_GATHER_GROUPS: the gather kernel for lone pinned rows,
   on, off, or with 1..16 workgroups;
 - QSMD5_PC_LANES and QSMD5_LOAD_NT: lanes per latency-kernel workgroup and nt
-  producer loads.
+  producer loads;
+- QSMD5_STAGING_BYTES / QSMD5_SLICE_BYTES: a staging ring of one or a few
+  regions and small slices, so that slices reuse regions behind the kernels
+  that last read them (the host-ordered pipeline's waits).
 Host chunks come from two separate pinned pools, a pageable pool and a
 pageable pool registered with qsmd5_register_host.
 This drives the paths the fixed tests pin one at a time: the inline small-batch
@@ -36,7 +39,8 @@ N_BATCH = int(os.environ.get("QSMD5_FUZZ_SEEDS", "64"))
 N_STREAM = max(16, N_BATCH // 4)
 EDGES = [0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128, 4095, 4096, 4097]
 KNOBS = ("QSMD5_COLUMN_BYTES", "QSMD5_KERNEL", "QSMD5_MAPS_AFTER", "QSMD5_GATHER",
-         "QSMD5_GATHER_GROUPS", "QSMD5_PC_LANES", "QSMD5_LOAD_NT")
+         "QSMD5_GATHER_GROUPS", "QSMD5_PC_LANES", "QSMD5_LOAD_NT", "QSMD5_STAGING_BYTES",
+         "QSMD5_SLICE_BYTES")
 
 
 @pytest.fixture(scope="module")
@@ -99,6 +103,10 @@ def test_random_batches(pools, seed):
         "QSMD5_GATHER_GROUPS": rng.choice([None, "1", "3", "16"]),
         "QSMD5_PC_LANES": rng.choice([None, None, "16", "32", "48"]),
         "QSMD5_LOAD_NT": rng.choice([None, None, "1"]),
+        # a ring of one or a few regions: slices wait for the kernel that
+        # last used their region (the host-ordered pipeline's reuse path)
+        "QSMD5_STAGING_BYTES": rng.choice([None, None, None, "1", str(1 << 20), str(8 << 20)]),
+        "QSMD5_SLICE_BYTES": rng.choice([None, None, "65536", str(1 << 20)]),
     }
     for k, v in env.items():
         if v is None:
