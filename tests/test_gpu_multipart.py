@@ -94,3 +94,24 @@ def test_pool_refilled_between_waves(gold, pool_kind):
     gathered = [int(ln.split(" regions, ")[1].split()[0]) for ln in r["_stderr"].splitlines()
                 if ln.startswith("qsmd5 trace:") and "gathered rows" in ln]
     assert len(gathered) == 4 and min(gathered) >= 64, gathered  # 2 passes x 2 waves, every row
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wait", ["auto", "spin"])
+def test_gpu_waves_leave_the_host_cores_free(gold, wait):
+    """A GPU wave is one ~85 ms chain; the caller used to spin through it and
+    the column pipeline's stream waits kept a HIP thread polling too (~2 host
+    cores per wave, profiles/r04_route_sweep_before_hostorder.jsonl).  With the
+    host-ordered staging and sleep-poll waits (QSMD5_WAIT=auto), 8 waves of 8
+    pinned 10 MiB parts cost the host little beyond the harness's own gather;
+    QSMD5_WAIT=spin still hashes correctly (and spins the caller)."""
+    r = run(["--aligned", "--size=%d" % (64 * 10 * MiB), "--pool=8", "--pinned", "--slab",
+             "--no-pipeline", "--repeat=2"], "gpu", extra_env={"QSMD5_WAIT": wait})
+    assert r["md5"] == gold[:64] and r["gpu_waves"] == 8
+    hashing_cpu = r["cpu_s_runs"][-1] - r["gather_s"]
+    print("QSMD5_WAIT=%s: wall %.3f s, host CPU beyond the gather %.3f s, busy threads %s"
+          % (wait, r["wall_s_runs"][-1], hashing_cpu, r["busy_threads"]))
+    if wait == "auto":
+        assert hashing_cpu < 0.15 * r["wall_s_runs"][-1], r
+    else:
+        assert hashing_cpu > 0.5 * r["hash_s"], r  # the spin is real: the test would see a regression
