@@ -1191,6 +1191,11 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
   // (a group's columns run one after another behind its copies), so the host
   // keeps polling, backing off from 20 us to 500 us.
   for (hipEvent_t t : tails) {
+    if (wait_mode() == 1 || wait_mode() == 2) {  // QSMD5_WAIT=block / spin: HIP's own wait
+      const hipError_t e = hipEventSynchronize(t);
+      if (e != hipSuccess) return drain(hip_fail(e, "waiting for the batch"));
+      continue;
+    }
     int idle_us = 20;
     for (;;) {
       const int q = landed(t);
