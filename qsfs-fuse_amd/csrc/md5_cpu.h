@@ -38,6 +38,11 @@ typedef bool (*MbPull)(void* ctx, uint32_t* i);
 bool mb16_available();
 void md5_mb16(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16], MbPull pull,
               void* ctx);
+// The same with 32 lanes: two 16-lane groups whose chains interleave, for
+// cores with the vector pipes to run both (the runtime times both once and
+// keeps the faster, qsmd5_runtime.cpp measure_cpu_rates).
+void md5_mb32(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16], MbPull pull,
+              void* ctx);
 
 // Streaming state: the MD5 class (update()* then final()), any piece sizes.
 struct Ctx {

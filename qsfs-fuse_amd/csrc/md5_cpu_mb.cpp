@@ -48,16 +48,22 @@ constexpr int kTern[4] = {0xCA /* F */, 0xE4 /* G */, 0x96 /* H */, 0x39 /* I */
 
 alignas(64) const uint8_t kZeroBlock[64] = {0};
 
-// Steps I..63 over 16 lanes; roles rotate as in md5_cpu.cpp.
-template <int I>
-QS_AVX512 inline void steps16(__m512i& a, __m512i& b, __m512i& c, __m512i& d, const __m512i* x) {
+// Steps I..63 over G groups of 16 lanes.  Register roles rotate every step,
+// as in md5_core.h: at step i the reference's "a" is v[(4 - i) & 3].  With
+// G = 2 the two groups' independent chains interleave, so that one group's
+// dependent ternlog/add/rotate/add fills the other's latency.
+template <int G, int I>
+QS_AVX512 inline void stepsG(__m512i (&v)[4][G], const __m512i (&x)[G][16]) {
   if constexpr (I < 64) {
-    // a + x + K does not wait for b: only ternlog, add, rotate, add are serial
-    const __m512i amk = _mm512_add_epi32(_mm512_add_epi32(a, x[word_of(I)]),
-                                         _mm512_set1_epi32((int)kT[I]));
-    const __m512i f = _mm512_ternarylogic_epi32(b, c, d, kTern[I >> 4]);
-    a = _mm512_add_epi32(b, _mm512_rol_epi32(_mm512_add_epi32(amk, f), kRot[I >> 4][I & 3]));
-    steps16<I + 1>(d, a, b, c, x);
+    constexpr int ia = (4 - (I & 3)) & 3, ib = (ia + 1) & 3, ic = (ia + 2) & 3, id = (ia + 3) & 3;
+    for (int g = 0; g < G; ++g) {
+      // a + x + K does not wait for b: only ternlog, add, rotate, add are serial
+      const __m512i amk = _mm512_add_epi32(_mm512_add_epi32(v[ia][g], x[g][word_of(I)]),
+                                           _mm512_set1_epi32((int)kT[I]));
+      const __m512i f = _mm512_ternarylogic_epi32(v[ib][g], v[ic][g], v[id][g], kTern[I >> 4]);
+      v[ia][g] = _mm512_add_epi32(v[ib][g], _mm512_rol_epi32(_mm512_add_epi32(amk, f), kRot[I >> 4][I & 3]));
+    }
+    stepsG<G, I + 1>(v, x);
   }
 }
 
@@ -104,24 +110,31 @@ void finish_scalar(uint32_t h[4], const uint8_t* tail, uint32_t rem, uint64_t le
   memcpy(out, h, 16);
 }
 
-QS_AVX512 void run16(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16],
-                     MbPull pull, void* ctx) {
-  const uint8_t* p[16];
-  uint64_t left[16];  // whole blocks still to run
-  uint32_t idx[16];
-  bool busy[16];
-  alignas(64) uint32_t s[4][16];
-  for (int l = 0; l < 16; ++l) {
+// 16 x G lanes, each holding one message, refilled from `pull` when its
+// message ends; every live lane runs the same number of whole blocks in
+// lockstep, then the lanes whose messages ended finish on the scalar path.
+template <int G>
+QS_AVX512 void runG(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16], MbPull pull,
+                    void* ctx) {
+  constexpr int L = 16 * G;
+  const uint8_t* p[L];
+  uint64_t left[L];  // whole blocks still to run
+  uint32_t idx[L];
+  bool busy[L];
+  alignas(64) uint32_t s[4][L];
+  for (int l = 0; l < L; ++l) {
     p[l] = kZeroBlock;
     left[l] = 0;
     busy[l] = false;
   }
-  __m512i A = _mm512_setzero_si512(), B = A, C = A, D = A;
+  __m512i S[4][G];
+  for (int k = 0; k < 4; ++k)
+    for (int g = 0; g < G; ++g) S[k][g] = _mm512_setzero_si512();
   bool more = true;  // the queue may still hold messages
   for (;;) {
     // refill idle lanes; messages shorter than one block finish right here
-    __mmask16 fresh = 0;
-    for (int l = 0; l < 16 && more; ++l) {
+    __mmask16 fresh[G] = {};
+    for (int l = 0; l < L && more; ++l) {
       while (!busy[l] && more) {
         uint32_t i;
         if (!pull(ctx, &i)) {
@@ -138,40 +151,41 @@ QS_AVX512 void run16(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (
         idx[l] = i;
         p[l] = ptrs[i];
         left[l] = nb;
-        fresh |= (__mmask16)(1u << l);
+        fresh[l / 16] |= (__mmask16)(1u << (l % 16));
       }
     }
-    A = _mm512_mask_mov_epi32(A, fresh, _mm512_set1_epi32((int)kIV[0]));
-    B = _mm512_mask_mov_epi32(B, fresh, _mm512_set1_epi32((int)kIV[1]));
-    C = _mm512_mask_mov_epi32(C, fresh, _mm512_set1_epi32((int)kIV[2]));
-    D = _mm512_mask_mov_epi32(D, fresh, _mm512_set1_epi32((int)kIV[3]));
-    __mmask16 live = 0;
+    for (int k = 0; k < 4; ++k)
+      for (int g = 0; g < G; ++g) S[k][g] = _mm512_mask_mov_epi32(S[k][g], fresh[g], _mm512_set1_epi32((int)kIV[k]));
+    __mmask16 live[G] = {};
+    bool any = false;
     uint64_t run = ~0ull;
-    for (int l = 0; l < 16; ++l)
+    for (int l = 0; l < L; ++l)
       if (busy[l]) {
-        live |= (__mmask16)(1u << l);
+        live[l / 16] |= (__mmask16)(1u << (l % 16));
+        any = true;
         run = left[l] < run ? left[l] : run;
       }
-    if (!live) return;
+    if (!any) return;
     // every live lane has `run` whole blocks: run them in lockstep (idle
     // lanes read a zero block and keep their registers)
     for (uint64_t j = 0; j < run; ++j) {
-      __m512i x[16];
-      load_transpose(x, p);
-      __m512i a = A, b = B, c = C, d = D;
-      steps16<0>(a, b, c, d, x);
-      A = _mm512_mask_add_epi32(A, live, A, a);
-      B = _mm512_mask_add_epi32(B, live, B, b);
-      C = _mm512_mask_add_epi32(C, live, C, c);
-      D = _mm512_mask_add_epi32(D, live, D, d);
-      for (int l = 0; l < 16; ++l)
+      __m512i x[G][16];
+      for (int g = 0; g < G; ++g) {
+        const uint8_t* const(&pg)[16] = *reinterpret_cast<const uint8_t* const(*)[16]>(p + 16 * g);
+        load_transpose(x[g], pg);
+      }
+      __m512i v[4][G];
+      for (int k = 0; k < 4; ++k)
+        for (int g = 0; g < G; ++g) v[k][g] = S[k][g];
+      stepsG<G, 0>(v, x);
+      for (int k = 0; k < 4; ++k)
+        for (int g = 0; g < G; ++g) S[k][g] = _mm512_mask_add_epi32(S[k][g], live[g], S[k][g], v[k][g]);
+      for (int l = 0; l < L; ++l)
         if (busy[l]) p[l] += 64;
     }
-    _mm512_store_si512((void*)s[0], A);
-    _mm512_store_si512((void*)s[1], B);
-    _mm512_store_si512((void*)s[2], C);
-    _mm512_store_si512((void*)s[3], D);
-    for (int l = 0; l < 16; ++l) {
+    for (int k = 0; k < 4; ++k)
+      for (int g = 0; g < G; ++g) _mm512_store_si512((void*)(s[k] + 16 * g), S[k][g]);
+    for (int l = 0; l < L; ++l) {
       if (!busy[l]) continue;
       left[l] -= run;
       if (left[l]) continue;
@@ -190,7 +204,12 @@ bool mb16_available() { return __builtin_cpu_supports("avx512f"); }
 
 void md5_mb16(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16], MbPull pull,
               void* ctx) {
-  run16(ptrs, lens, out, pull, ctx);
+  runG<1>(ptrs, lens, out, pull, ctx);
+}
+
+void md5_mb32(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16], MbPull pull,
+              void* ctx) {
+  runG<2>(ptrs, lens, out, pull, ctx);
 }
 
 }  // namespace cpu

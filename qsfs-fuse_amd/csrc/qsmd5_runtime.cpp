@@ -1651,7 +1651,8 @@ double env_gibs(const char* name) {
 // This host's CPU MD5 rates, timed once (see above).
 struct CpuRates {
   double chain = kCpuChainGiBs;  // one thread, one scalar chain
-  double lane_thread = 0;        // one thread, 16 AVX-512 lanes together (0: no AVX-512F)
+  double lane_thread = 0;        // one thread, its AVX-512 lanes together (0: no AVX-512F)
+  int mb_groups = 1;             // 16-lane groups per thread that timed faster (1 or 2)
   bool measured = false;
 };
 
@@ -1701,6 +1702,36 @@ CpuRates measure_cpu_rates() {
       qsmd5::cpu::md5_mb16(ptrs, lens, out, Pull::take, &p);
     });
     if (t_mb > 0) r.lane_thread = (double)kBytes / t_mb / kGiB;
+    // 32 messages of 4 KiB in two interleaved 16-lane groups: whether this
+    // core's vector pipes run two groups faster than one (QSMD5_CPU_MB_GROUPS
+    // = 1 / 2 forces the choice)
+    constexpr uint32_t kLanes2 = 32;
+    const uint8_t* ptrs2[kLanes2];
+    uint64_t lens2[kLanes2];
+    uint8_t out2[kLanes2][16];
+    for (uint32_t i = 0; i < kLanes2; ++i) {
+      ptrs2[i] = buf.get() + i * (kBytes / kLanes2);
+      lens2[i] = kBytes / kLanes2;
+    }
+    struct Pull2 {
+      uint32_t next = 0;
+      static bool take(void* ctx, uint32_t* i) {
+        Pull2* p = static_cast<Pull2*>(ctx);
+        if (p->next >= kLanes2) return false;
+        *i = p->next++;
+        return true;
+      }
+    };
+    const double t_mb2 = best_of_3([&] {
+      Pull2 p;
+      qsmd5::cpu::md5_mb32(ptrs2, lens2, out2, Pull2::take, &p);
+    });
+    const uint64_t forced = env_u64("QSMD5_CPU_MB_GROUPS", 0);
+    const bool two = forced ? forced == 2 : (t_mb2 > 0 && t_mb > 0 && t_mb2 < 0.95 * t_mb);
+    if (two) {
+      r.mb_groups = 2;
+      if (t_mb2 > 0) r.lane_thread = (double)kBytes / t_mb2 / kGiB;
+    }
   }
   return r;
 }
@@ -1793,8 +1824,10 @@ bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
   const bool lanes = lanes_priced(chunks, n, flags);  // only for all-host batches
   auto cpu_ms_of = [&](uint64_t d2h) {
     if (!lanes) return cpu_est_ms(longest, total, d2h);
-    const double lt = cpu_rates().lane_thread;
-    return 1e3 * std::max((double)longest / (lt / 16.0), (double)total / ((double)cpu_threads() * lt)) / kGiB;
+    const double lt = cpu_rates().lane_thread;  // a lane's chain: 1/(16 x groups) of it
+    const double lanes_per_thread = 16.0 * cpu_rates().mb_groups;
+    return 1e3 * std::max((double)longest / (lt / lanes_per_thread),
+                          (double)total / ((double)cpu_threads() * lt)) / kGiB;
   };
   if (!(cpu_ms_of(0) < gpu_est_ms(longest, total))) return false;
   if (lanes || (flags & QSMD5_FLAG_HOST) || qsmd5_device_count() <= 0) return true;
@@ -1931,6 +1964,11 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   // vector pipes), so the lanes pay once a thread has 2 or more chunks.
   const bool mb = allow_mb && n_host >= 2 * std::min<size_t>(cpu_threads(), n) &&
                   env_u64("QSMD5_CPU_MB", 1) && qsmd5::cpu::mb16_available();
+  // two interleaved 16-lane groups per thread where this core runs them
+  // faster (timed once, CpuRates::mb_groups) and there are messages to fill
+  // more than one group per thread
+  const bool mb32 = mb && cpu_rates().mb_groups == 2 &&
+                    n_host > 16 * std::min<size_t>(cpu_threads(), n);
   std::vector<const uint8_t*> ptrs;
   if (mb) {
     ptrs.resize(n);
@@ -1970,7 +2008,8 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
       MbQueue q{&next, n, order.data(), on_dev.data(), &hip_err,
                 [](void* self, uint32_t i) { return static_cast<Worker*>(self)->device_chunk(i); },
                 &w};
-      qsmd5::cpu::md5_mb16(ptrs.data(), len.data(), digests, mb_pull, &q);
+      if (mb32) qsmd5::cpu::md5_mb32(ptrs.data(), len.data(), digests, mb_pull, &q);
+      else qsmd5::cpu::md5_mb16(ptrs.data(), len.data(), digests, mb_pull, &q);
       return;
     }
     for (size_t k; (k = next.fetch_add(1)) < n && hip_err.load() == (int)hipSuccess;) {
