@@ -1653,6 +1653,7 @@ struct CpuRates {
   double chain = kCpuChainGiBs;  // one thread, one scalar chain
   double lane_thread = 0;        // one thread, its AVX-512 lanes together (0: no AVX-512F)
   int mb_groups = 1;             // 16-lane groups per thread that timed faster (1 or 2)
+  double lane16 = 0, lane32 = 0;  // one thread's rate with 16 / 32 lanes busy
   bool measured = false;
 };
 
@@ -1701,7 +1702,7 @@ CpuRates measure_cpu_rates() {
       Pull p;
       qsmd5::cpu::md5_mb16(ptrs, lens, out, Pull::take, &p);
     });
-    if (t_mb > 0) r.lane_thread = (double)kBytes / t_mb / kGiB;
+    if (t_mb > 0) r.lane_thread = r.lane16 = (double)kBytes / t_mb / kGiB;
     // 32 messages of 4 KiB in two interleaved 16-lane groups: whether this
     // core's vector pipes run two groups faster than one (QSMD5_CPU_MB_GROUPS
     // = 1 / 2 forces the choice)
@@ -1726,11 +1727,15 @@ CpuRates measure_cpu_rates() {
       Pull2 p;
       qsmd5::cpu::md5_mb32(ptrs2, lens2, out2, Pull2::take, &p);
     });
+    if (t_mb2 > 0) r.lane32 = (double)kBytes / t_mb2 / kGiB;
     const uint64_t forced = env_u64("QSMD5_CPU_MB_GROUPS", 0);
-    const bool two = forced ? forced == 2 : (t_mb2 > 0 && t_mb > 0 && t_mb2 < 0.95 * t_mb);
+    if (forced == 1) r.lane32 = 0;  // never two groups
+    const bool two = forced ? forced == 2 : (r.lane32 > 0 && r.lane16 > 0 && r.lane32 > 1.05 * r.lane16);
     if (two) {
       r.mb_groups = 2;
-      if (t_mb2 > 0) r.lane_thread = (double)kBytes / t_mb2 / kGiB;
+      if (r.lane32 > 0) r.lane_thread = r.lane32;
+    } else {
+      r.lane32 = 0;
     }
   }
   return r;
@@ -1964,11 +1969,29 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
   // vector pipes), so the lanes pay once a thread has 2 or more chunks.
   const bool mb = allow_mb && n_host >= 2 * std::min<size_t>(cpu_threads(), n) &&
                   env_u64("QSMD5_CPU_MB", 1) && qsmd5::cpu::mb16_available();
-  // two interleaved 16-lane groups per thread where this core runs them
-  // faster (timed once, CpuRates::mb_groups) and there are messages to fill
-  // more than one group per thread
-  const bool mb32 = mb && cpu_rates().mb_groups == 2 &&
-                    n_host > 16 * std::min<size_t>(cpu_threads(), n);
+  // Two interleaved 16-lane groups per thread where this core runs them
+  // faster (timed once, CpuRates) and the batch fills 32 lanes on every
+  // thread -- and only if the estimate says so: a lane of 32 runs its chain
+  // slower than a lane of 16 (EPYC 9575F: 10.2 GiB/s over 32 lanes against
+  // 6.7 over 16 per thread), so a batch dominated by one long chunk (config
+  // 4's 64 MiB) is faster on 16 (profiles/r04_cpu_mb_groups.log).
+  bool mb32 = false;
+  if (mb && cpu_rates().mb_groups == 2 && cpu_rates().lane32 > 0 && cpu_rates().lane16 > 0) {
+    const double T = (double)std::min<size_t>(cpu_threads(), n);
+    if ((double)n_host >= 32.0 * T) {
+      uint64_t longest = 0, host_total = 0;
+      for (size_t i = 0; i < n; ++i)
+        if (!on_dev[i]) {
+          longest = std::max(longest, len[i]);
+          host_total += len[i];
+        }
+      auto est = [&](double rate, double lanes) {
+        return std::max((double)longest / (rate / lanes), (double)host_total / (T * rate));
+      };
+      static const bool forced2 = env_u64("QSMD5_CPU_MB_GROUPS", 0) == 2;  // tests: always
+      mb32 = forced2 || est(cpu_rates().lane32, 32.0) < est(cpu_rates().lane16, 16.0);
+    }
+  }
   std::vector<const uint8_t*> ptrs;
   if (mb) {
     ptrs.resize(n);

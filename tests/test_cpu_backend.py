@@ -329,9 +329,11 @@ def test_product_library_does_not_carry_the_oracle():
 
 
 def test_multibuffer_and_scalar_paths_agree():
-    """Both CPU paths against the oracle, each in its own process: the AVX-512
-    multi-buffer lanes (md5_cpu_mb.cpp, when the host has AVX-512F) and the
-    scalar chain (QSMD5_CPU_MB=0).  Ragged lengths 0..3 MiB at odd offsets, so
+    """Every CPU path against the oracle, each in its own process: the AVX-512
+    multi-buffer lanes (md5_cpu_mb.cpp, when the host has AVX-512F) in one
+    16-lane group per thread and in two interleaved groups (32 lanes,
+    QSMD5_CPU_MB_GROUPS=2: 200 chunks on 3 threads fill them), and the scalar
+    chain (QSMD5_CPU_MB=0).  Ragged lengths 0..3 MiB at odd offsets, so
     lanes run out at different blocks and are refilled mid-batch, plus tails
     on every side of the 56-byte padding edge."""
     script = r'''
@@ -351,8 +353,8 @@ got = qsmd5.hash_batch(chunks, flags=qsmd5.FLAG_CPU_ONLY)
 assert got == md5_many(chunks), "CPU backend digests differ from the oracle"
 print("ok", len(chunks))
 ''' % (os.path.join(ROOT, "qsfs-fuse_amd"), os.path.join(ROOT, "tests"))
-    for mb in ("1", "0"):
-        env = dict(os.environ, QSMD5_CPU_MB=mb, QSMD5_CPU_THREADS="3")
+    for mb, groups in (("1", "1"), ("1", "2"), ("0", "1")):  # 16 lanes, 32 lanes, scalar
+        env = dict(os.environ, QSMD5_CPU_MB=mb, QSMD5_CPU_THREADS="3", QSMD5_CPU_MB_GROUPS=groups)
         out = subprocess.run([os.sys.executable, "-c", script], env=env, capture_output=True,
                              text=True, timeout=300)
         assert out.returncode == 0 and out.stdout.startswith("ok"), (mb, out.stdout + out.stderr[-2000:])
