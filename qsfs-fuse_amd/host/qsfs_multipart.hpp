@@ -53,6 +53,7 @@
 #include <mutex>
 #include <stdexcept>
 #include <string>
+#include <system_error>
 #include <vector>
 
 #include "qsfs_md5.hpp"
