@@ -79,16 +79,20 @@ def _run(script, **env):
     return subprocess.run([PY, "-c", script], env=e, capture_output=True, text=True, timeout=300)
 
 
-def test_two_contexts_shard_and_match_oracle():
-    out = _run(SHARD_SCRIPT, QSMD5_DEVICES="0,0", QSMD5_SHARD_BYTES=str(8 << 20),
+@pytest.mark.parametrize("devices", ["0,0", "0,0,0,0"])
+def test_contexts_shard_and_match_oracle(devices):
+    """Two contexts, and four (the node's shard threads rehearsed on one
+    card): every context takes a shard of some batch, each runs the
+    host-ordered staging pipeline on its own streams, every digest matches."""
+    out = _run(SHARD_SCRIPT, QSMD5_DEVICES=devices, QSMD5_SHARD_BYTES=str(8 << 20),
                QSMD5_TRACE="1")
     assert out.returncode == 0, out.stdout + out.stderr[-4000:]
     assert "shard-ok" in out.stdout
-    # the split really happened: both contexts took chunks in some batch
+    # the split really happened: every context took chunks in some batch
     shards = [l for l in out.stderr.splitlines() if l.startswith("qsmd5 shard:")]
-    assert any("context 1 (GPU 0) takes" in l and not l.endswith("takes 0 chunks") for l in shards), \
-        "\n".join(shards)
-    assert any("context 0 (GPU 0) takes" in l and not l.endswith("takes 0 chunks") for l in shards)
+    for c in range(len(devices.split(","))):
+        assert any("context %d (GPU 0) takes" % c in l and not l.endswith("takes 0 chunks")
+                   for l in shards), "\n".join(shards)
 
 
 def test_small_batch_stays_on_one_gpu():
