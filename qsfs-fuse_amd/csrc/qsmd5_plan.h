@@ -242,4 +242,66 @@ inline std::vector<uint32_t> plan_shards(const std::vector<uint64_t>& host_len, 
   return shard;
 }
 
+// The host-ordered staging schedule (qsmd5_runtime.cpp run_batch): S slices,
+// nregions ring regions (slice si fills region si % nregions), the copies of
+// slice si enqueued at most after the host has seen the kernel of slice
+// si - nregions finish (its region is then free), the kernel of slice si
+// launched only after the host has seen slice si's copies land, and slices
+// with gather rows (read from the metadata block) copied only once that
+// block has landed (`meta`).  pipeline_turn runs one turn: the copies of at
+// most one slice (a pageable copy is staged by HIP on the calling thread, so
+// kernels go out between copies), then every kernel that is ready, in slice
+// order.  Returns 1 if anything was enqueued, 0 if the host must wait, -1 if
+// a callback failed.  Callbacks:
+//   copy_landed(si) / kernel_done(si): 1 yes, 0 not yet, -1 error;
+//   needs_meta(si): the slice has gather rows;
+//   enqueue_copies(si) / launch(si): 0 or an error code.
+// tests/cpp/test_plan.cpp drives it against simulated engines with random
+// completion times: every order is respected, every slice runs, no stall.
+struct PipelineState {
+  size_t nc = 0;  // slices whose copies are enqueued
+  size_t nk = 0;  // slices whose kernels are launched
+  int err = 0;    // the failing callback's code, when a turn returns -1
+};
+
+template <class CopyLanded, class KernelDone, class NeedsMeta, class EnqueueCopies, class Launch>
+inline int pipeline_turn(size_t S, size_t nregions, bool meta, PipelineState& st,
+                         CopyLanded&& copy_landed, KernelDone&& kernel_done, NeedsMeta&& needs_meta,
+                         EnqueueCopies&& enqueue_copies, Launch&& launch) {
+  bool moved = false;
+  if (st.nc < S) {
+    bool ok = true;
+    if (st.nc >= nregions) {  // its region: free once the host saw the last user's kernel end
+      if (st.nc - nregions >= st.nk) {
+        ok = false;  // that kernel is not even launched yet
+      } else {
+        const int q = kernel_done(st.nc - nregions);
+        if (q < 0) return -1;
+        ok = q == 1;
+      }
+    }
+    if (ok && needs_meta(st.nc) && !meta) ok = false;
+    if (ok) {
+      if (int rc = enqueue_copies(st.nc)) {
+        st.err = rc;
+        return -1;
+      }
+      ++st.nc;
+      moved = true;
+    }
+  }
+  while (st.nk < st.nc && meta) {
+    const int q = copy_landed(st.nk);
+    if (q < 0) return -1;
+    if (!q) break;
+    if (int rc = launch(st.nk)) {
+      st.err = rc;
+      return -1;
+    }
+    ++st.nk;
+    moved = true;
+  }
+  return moved ? 1 : 0;
+}
+
 }  // namespace qsmd5

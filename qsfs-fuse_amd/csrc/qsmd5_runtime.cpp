@@ -1126,45 +1126,28 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       if (int rc = launch_slice(0, s0)) return drain(rc);
     }
   } else {
-    size_t nc = 0, nk = 0;  // slices whose copies / kernels are enqueued
-    bool meta = false;      // the metadata block (descriptors, gather rows) has landed
+    qsmd5::PipelineState st;
+    bool meta = false;  // the metadata block (descriptors, gather rows) has landed
     int idle_us = 20;
-    while (nk < S) {
-      bool moved = false;
+    while (st.nk < S) {
       if (!meta) {
         const int q = landed(r.ev_meta);
         if (q < 0) return drain(-EIO);
         meta = q == 1;
       }
-      // one slice's copies per turn, then whatever kernels are ready: a
-      // pageable source makes HIP stage the copy on this thread before the
-      // call returns, and the kernels of the slices before it must not wait
-      // for all of that
-      do {
-        if (nc >= S) break;
-        if (nc >= nregions) {  // its region: free once the host saw the last user's kernel end
-          if (nc - nregions >= nk) break;  // that kernel is not even launched yet
-          const int q = landed(done[nc - nregions]);
-          if (q < 0) return drain(-EIO);
-          if (!q) break;
-        }
-        if (slice_gathers(nc) && !meta) break;  // the gather kernel reads rows from the meta block
-        if (int rc = enqueue_copies(nc, r.copy[nc % r.ncopy])) return drain(rc);
-        ++nc;
-        moved = true;
-      } while (false);
-      while (nk < nc && meta) {
-        const int q = landed(copied[nk]);
-        if (q < 0) return drain(-EIO);
-        if (!q) break;
-        const int csi = compute_stream_of(nk);
-        used |= 1u << csi;
-        if (int rc = launch_slice(nk, r.compute[csi])) return drain(rc);
-        ++nk;
-        moved = true;
-      }
-      if (nk == S) break;
-      if (moved) {
+      const int t = qsmd5::pipeline_turn(
+          S, nregions, meta, st, [&](size_t si) { return landed(copied[si]); },
+          [&](size_t si) { return landed(done[si]); },
+          [&](size_t si) { return slice_gathers(si) != 0; },
+          [&](size_t si) { return enqueue_copies(si, r.copy[si % r.ncopy]); },
+          [&](size_t si) {
+            const int csi = compute_stream_of(si);
+            used |= 1u << csi;
+            return launch_slice(si, r.compute[csi]);
+          });
+      if (t < 0) return drain(st.err ? st.err : -EIO);
+      if (st.nk == S) break;
+      if (t > 0) {
         idle_us = 20;
       } else {
         std::this_thread::sleep_for(std::chrono::microseconds(idle_us));

@@ -14,6 +14,8 @@
 //      and when automatic a multiple of 64 KiB, >= kColMin, with at most
 //      kColMaxPerChunk (+1) columns per chunk;
 //   6. number the segment descriptors of multi-column groups densely (nseg);
+// the host-ordered staging schedule (pipeline_turn) must respect every
+// copy/kernel/region order against simulated engines and never stall;
 // and the multi-GPU split (plan_shards) must give contiguous shards, on
 // k = min(#GPUs, max(ceil(bytes / shard_bytes), ceil(parts / resident))) GPUs,
 // each within one chunk of an equal share of the bytes.
@@ -282,6 +284,82 @@ static int run_copy_run_cases(std::mt19937_64& rng) {
   return cases;
 }
 
+// The host-ordered staging schedule (pipeline_turn) against simulated
+// engines: ncopy copy streams and some compute streams, each running its
+// queue in order with random durations; the metadata block lands at a random
+// time.  The host calls pipeline_turn; when a turn enqueues nothing, time
+// moves to the next completion (no completion pending = a stall).  Checked:
+// a slice's copies are enqueued only after the kernel that last used its
+// region has finished, and only after the metadata block has landed if the
+// slice has gather rows; its kernel only after its copies have landed and the
+// metadata block too; kernels in slice order; every slice runs.
+static int run_pipeline_cases(std::mt19937_64& rng) {
+  int cases = 0;
+  for (int t = 0; t < 3000; ++t) {
+    const size_t S = 1 + rng() % 120;
+    const size_t nregions = 1 + rng() % (S + 2);
+    const size_t R = std::min(nregions, S);
+    const int ncopy = 1 + (int)(rng() % 4), ncomp = 1 + (int)(rng() % 7);
+    std::vector<int> group(S);
+    for (size_t si = 0; si < S; ++si) group[si] = (int)(rng() % ncomp);
+    std::vector<bool> gathers(S);
+    for (size_t si = 0; si < S; ++si) gathers[si] = rng() % 5 == 0;
+    const double meta_at = (double)(rng() % 50);
+    double now = 0;
+    std::vector<double> copy_end(S, -1), kern_end(S, -1);
+    std::vector<double> copy_stream_free(ncopy, 0), comp_stream_free(ncomp, 0);
+    auto done_by = [&](double end) { return end >= 0 && end <= now; };
+    PipelineState st;
+    size_t launched_before = 0;
+    bool stalled = false;
+    for (int turns = 0; st.nk < S; ++turns) {
+      const bool meta = now >= meta_at;
+      const int r = pipeline_turn(
+          S, R, meta, st, [&](size_t si) { return done_by(copy_end[si]) ? 1 : 0; },
+          [&](size_t si) { return done_by(kern_end[si]) ? 1 : 0; },
+          [&](size_t si) { return gathers[si] ? true : false; },
+          [&](size_t si) {
+            CHECK(si < R || done_by(kern_end[si - R]),
+                  "case %d: copies of slice %zu before the kernel of slice %zu (its region) ended", t, si,
+                  si - R);
+            CHECK(!gathers[si] || meta, "case %d: gather rows of slice %zu before the metadata", t, si);
+            const int cs = (int)(si % ncopy);
+            const double start = std::max(now, copy_stream_free[cs]);
+            copy_end[si] = copy_stream_free[cs] = start + 1 + (double)(rng() % 20);
+            return 0;
+          },
+          [&](size_t si) {
+            CHECK(done_by(copy_end[si]), "case %d: kernel of slice %zu before its copies landed", t, si);
+            CHECK(meta, "case %d: kernel of slice %zu before the metadata landed", t, si);
+            CHECK(si == launched_before, "case %d: kernel %zu out of order", t, si);
+            ++launched_before;
+            const int k = group[si];
+            const double start = std::max(now, comp_stream_free[k]);
+            kern_end[si] = comp_stream_free[k] = start + 1 + (double)(rng() % 30);
+            return 0;
+          });
+      CHECK(r >= 0, "case %d: turn failed", t);
+      if (r > 0) continue;
+      // the host waits: the next completion (a copy, a kernel, the metadata)
+      double next = 1e300;
+      for (size_t si = 0; si < S; ++si) {
+        if (copy_end[si] > now) next = std::min(next, copy_end[si]);
+        if (kern_end[si] > now) next = std::min(next, kern_end[si]);
+      }
+      if (!meta) next = std::min(next, meta_at);
+      if (next == 1e300 || turns > 100000) {
+        stalled = true;
+        break;
+      }
+      now = next;
+    }
+    CHECK(!stalled, "case %d: S=%zu nregions=%zu stalled at nc=%zu nk=%zu", t, S, R, st.nc, st.nk);
+    CHECK(st.nc == S && st.nk == S, "case %d: not every slice ran", t);
+    ++cases;
+  }
+  return cases;
+}
+
 int main() {
   const uint64_t MiB = 1ull << 20, GiB = 1ull << 30;
   std::mt19937_64 rng(1234);
@@ -352,6 +430,7 @@ int main() {
         }
   }
   cases += run_copy_run_cases(rng);
+  cases += run_pipeline_cases(rng);
   printf("plan %s %d cases\n", fails ? "FAIL" : "ok", cases);
   return fails ? 1 : 0;
 }
