@@ -193,7 +193,7 @@ struct Dev {
   HostPinned h_meta, h_dig;
   // Per-batch events, reused (batches on one Dev are serialised by mu).
   hipEvent_t ev_meta = nullptr, ev_first = nullptr, ev_last = nullptr;
-  hipEvent_t ev_done = nullptr;  // hipEventBlockingSync: the host sleeps on long batches
+  hipEvent_t ev_done = nullptr;  // end of a batch, polled by a sleeping caller (wait_stream)
   uint64_t staging_cap = kDefaultStaging;
   double last_wall_ms = 0, last_kernel_ms = 0;
   std::atomic<uint32_t> chain_samples{0};  // batches that qualified as a chain-rate sample
