@@ -218,6 +218,12 @@ QSMD5_API int qsmd5_ctx_create(qsmd5_ctx** out);
 QSMD5_API int qsmd5_ctx_update(qsmd5_ctx* ctx, const void* ptr, uint64_t len);
 QSMD5_API int qsmd5_ctx_final(qsmd5_ctx* ctx, uint8_t digest[16]);
 QSMD5_API void qsmd5_ctx_destroy(qsmd5_ctx* ctx);
+/* A copy of a context with its running state (the reference MD5 is a value
+ * type: MD5.h:51-93 has the implicit copy members and operator<< takes it by
+ * value, MD5.h:61).  The copy and the original then update and finalise
+ * independently; a finalised or failed context copies as such.  Destroy the
+ * copy with qsmd5_ctx_destroy. */
+QSMD5_API int qsmd5_ctx_copy(const qsmd5_ctx* src, qsmd5_ctx** out);
 
 /* Pinned (page-locked) host buffers for the transfer-buffer pool
  * (ResourceManager, src/data/ResourceManager.cpp:53-77): the page gather

@@ -2670,6 +2670,49 @@ int qsmd5_ctx_create(qsmd5_ctx** out) {
   });
 }
 
+// The reference MD5 is a value type (MD5.h:51-93 declares no copy members, and
+// operator<< takes it by value, MD5.h:61): a copy carries the running state,
+// and the two then hash on independently.  A GPU context's state is copied
+// device to device; its pending tail bytes live on the host.
+int qsmd5_ctx_copy(const qsmd5_ctx* src, qsmd5_ctx** out) {
+  return guarded([&] {
+    if (!src || !out) return fail(-EINVAL, "qsmd5: NULL ctx/out");
+    *out = nullptr;
+    qsmd5_ctx* c = new qsmd5_ctx;
+    c->on_cpu = src->on_cpu;
+    c->failed = src->failed;
+    c->cpu = src->cpu;
+    c->hashed = src->hashed;
+    memcpy(c->tail, src->tail, sizeof c->tail);
+    c->tail_len = src->tail_len;
+    c->total = src->total;
+    c->finalized = src->finalized;
+    memcpy(c->digest, src->digest, sizeof c->digest);
+    if (src->on_cpu) {
+      *out = c;
+      return 0;
+    }
+    if (int rc = ensure_init()) {
+      delete c;
+      return rc;
+    }
+    std::lock_guard<std::mutex> lk(primary().mu);  // src's updates run under it
+    hipStream_t s = primary().compute[0];
+    hipError_t e = hipMalloc(&c->d_state, 16);
+    if (e == hipSuccess) e = hipMalloc(&c->d_tail, 64);
+    if (e == hipSuccess) e = hipMalloc(&c->d_seg, 64);
+    if (e == hipSuccess) e = hipMemsetAsync(c->d_seg, 0, 64, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(c->d_state, src->d_state, 16, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+      qsmd5_ctx_destroy(c);
+      return hip_fail(e, "qsmd5_ctx_copy");
+    }
+    *out = c;
+    return 0;
+  });
+}
+
 void qsmd5_ctx_destroy(qsmd5_ctx* c) {
   if (!c) return;
   CallScope call;  // its device buffers are freed before a shutdown tears HIP down

@@ -218,13 +218,37 @@ class MD5 {
     update(text.c_str(), static_cast<size_type>(text.length()));
     finalize();
   }
-  MD5(const MD5&) = delete;
-  MD5& operator=(const MD5&) = delete;
+  // A value type, as the reference's (implicit copy members; operator<< takes
+  // it by value, MD5.h:61): a copy carries the running state and then hashes
+  // on by itself (qsmd5_ctx_copy).
+  MD5(const MD5& o) : finalized_(o.finalized_) {
+    std::memcpy(digest_, o.digest_, 16);
+    if (o.ctx_) detail::check(qsmd5_ctx_copy(o.ctx_, &ctx_), "qsmd5_ctx_copy");
+  }
+  MD5& operator=(const MD5& o) {
+    if (this != &o) {
+      MD5 tmp(o);
+      swap(tmp);
+    }
+    return *this;
+  }
   MD5(MD5&& o) noexcept : ctx_(o.ctx_), finalized_(o.finalized_) {
     std::memcpy(digest_, o.digest_, 16);
     o.ctx_ = nullptr;
   }
+  MD5& operator=(MD5&& o) noexcept {
+    swap(o);
+    return *this;
+  }
   ~MD5() { qsmd5_ctx_destroy(ctx_); }
+  void swap(MD5& o) noexcept {
+    std::swap(ctx_, o.ctx_);
+    std::swap(finalized_, o.finalized_);
+    uint8_t t[16];
+    std::memcpy(t, digest_, 16);
+    std::memcpy(digest_, o.digest_, 16);
+    std::memcpy(o.digest_, t, 16);
+  }
 
   // After finalize() the reference's update() folds the bytes into a state
   // nobody reads again (finalize zeroised the count, MD5.cpp:306-309, and
@@ -260,6 +284,7 @@ class MD5 {
 // The reference declares md5() at global scope (MD5.h:95-96); so does this
 // drop-in, unless QSMD5_NO_GLOBAL_MD5 is defined.
 inline std::string md5(const std::string& str) { return qsmd5::md5(str); }
+using MD5 = qsmd5::MD5;  // the reference's class, global as in MD5.h:51
 template <class StreamPtr, qsmd5::detail::if_stream_ptr<StreamPtr> = 0>
 inline std::string md5(const StreamPtr& stream) {
   return qsmd5::md5(stream);

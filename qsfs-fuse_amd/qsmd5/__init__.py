@@ -130,6 +130,7 @@ def lib():
         "qsmd5_ctx_update": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]),
         "qsmd5_ctx_final": (ctypes.c_int, [ctypes.c_void_p, c_u8p]),
         "qsmd5_ctx_destroy": (None, [ctypes.c_void_p]),
+        "qsmd5_ctx_copy": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
         "qsmd5_alloc_pinned": (ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
         "qsmd5_free_pinned": (ctypes.c_int, [ctypes.c_void_p]),
         "qsmd5_register_host": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t]),
@@ -397,6 +398,17 @@ class MD5(object):
         p, L = _as_chunk(data, keep)
         _check(lib().qsmd5_ctx_update(self._ctx, p, L), "qsmd5_ctx_update")
         return self
+
+    def copy(self):
+        """An independent copy with the running state (the reference class is a
+        value type, MD5.h:51-93); as hashlib's copy()."""
+        other = MD5.__new__(MD5)
+        other._ctx = ctypes.c_void_p()
+        _check(lib().qsmd5_ctx_copy(self._ctx, ctypes.byref(other._ctx)), "qsmd5_ctx_copy")
+        other._digest = self._digest
+        return other
+
+    __copy__ = copy
 
     def finalize(self):
         if self._digest is None:

@@ -135,6 +135,31 @@ int main() {
     one.finalize();
     expect(one.hexdigest() == "900150983cd24fb0d6963f7d28e17f72", "update after finalize is a no-op");
   }
+  // 4b. The class is a value type, global as the reference's (MD5.h:51): a
+  //     copy taken mid-stream hashes on by itself; copy-assignment, moves and
+  //     operator<< by value (MD5.h:61) as any caller of the reference may use.
+  {
+    std::vector<char> d = lcg(31337, 5000);
+    MD5 a;
+    a.update(d.data(), 100);  // 100 B: one block hashed, 36 B pending in the tail
+    MD5 b(a);
+    b.update(d.data() + 100, 4900);
+    a.update("x", 1);
+    MD5 c;
+    c = b;  // copy-assign a live context over a fresh one
+    b.finalize();
+    c.update("y", 1);
+    std::printf("copy_b %s\n", b.hexdigest().c_str());
+    std::printf("copy_a %s\n", a.finalize().hexdigest().c_str());
+    std::printf("copy_c %s\n", c.finalize().hexdigest().c_str());
+    MD5 moved(std::move(c));
+    std::ostringstream os;
+    auto by_value = [&os](MD5 m) { os << m; };  // the reference's operator<<(ostream&, MD5)
+    by_value(moved);
+    expect(os.str() == moved.hexdigest(), "a copied finalised MD5 prints its digest");
+    MD5 fin(b);
+    expect(fin.hexdigest() == b.hexdigest(), "a copy of a finalised MD5 keeps the digest");
+  }
   // 5. Batch forms: md5_batch over ragged buffers, md5_file_parts over a
   //    25 MiB + 3 B "file" (PrepareUpload: 10, 10, 5 MiB + 3 B) and a 21 MiB one
   //    (10 MiB, then the 11 MiB remainder averaged into two 5.5 MiB parts).

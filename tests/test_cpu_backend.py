@@ -72,6 +72,13 @@ def test_stream_pieces_class(golden, monkeypatch):
         assert h.finalize().hexdigest() == case["md5"]
 
 
+def test_md5_copy_forks_the_state(monkeypatch):
+    """qsmd5_ctx_copy on a CPU context: the reference MD5's value semantics."""
+    monkeypatch.setenv("QSMD5_BACKEND", "cpu")
+    from md5_copy_cases import run_copy_cases
+    run_copy_cases(qsmd5, lambda d, off, n: d[off:off + n])
+
+
 def test_ragged_and_sweep(golden):
     g = golden("ragged.json")
     bufs = [lcg_bytes(7000 + i, L) for i, L in enumerate(g["lengths"])]

@@ -348,6 +348,21 @@ def test_stream_pieces_class(golden):
     assert qsmd5.MD5("abc").hexdigest() == "900150983cd24fb0d6963f7d28e17f72"
 
 
+def test_md5_copy_forks_the_state_on_gpu():
+    """qsmd5_ctx_copy on a GPU context (QSMD5_BACKEND=gpu: the chaining state
+    lives in device memory and is copied device to device), from host pieces
+    and from device pieces."""
+    from md5_copy_cases import run_copy_cases
+    run_copy_cases(qsmd5, lambda d, off, n: d[off:off + n])
+    dev = {}
+
+    def dev_piece(d, off, n):
+        if id(d) not in dev:
+            dev[id(d)] = torch.frombuffer(bytearray(d), dtype=torch.uint8).cuda()
+        return dev[id(d)][off:off + n]
+    run_copy_cases(qsmd5, dev_piece)
+
+
 def test_md5_stream_mirror():
     import io
     s = io.BytesIO(b"0123456789" * 1000)

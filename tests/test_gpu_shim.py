@@ -15,8 +15,6 @@ import pytest
 from conftest import ROOT
 from oracle_util import lcg_bytes
 
-pytestmark = pytest.mark.gpu
-
 BIN = os.path.join(ROOT, "tests", "cpp", "test_shim")
 
 
@@ -27,13 +25,7 @@ def build_shim():
         "-lqsmd5", "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-o", BIN])
 
 
-def test_cpp_dropin_shim():
-    torch = pytest.importorskip("torch")
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    if not os.path.exists(BIN):
-        build_shim()
-    out = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
+def check_shim_output(out):
     assert out.returncode == 0, out.stdout + out.stderr
     got = dict(line.split() for line in out.stdout.strip().splitlines() if not line.startswith("parts_"))
     h = lambda b: hashlib.md5(b).hexdigest()
@@ -60,4 +52,32 @@ def test_cpp_dropin_shim():
         for r in mine:
             off, sz = int(r[1]), int(r[2])
             assert r[3] == h(data[off:off + sz]), r
+    d = bytes(lcg_bytes(31337, 5000))
+    assert got["copy_b"] == h(d)
+    assert got["copy_a"] == h(d[:100] + b"x")
+    assert got["copy_c"] == h(d + b"y")
     assert got["failures"] == "0"
+
+
+def shim_binary():
+    src = os.path.join(ROOT, "tests", "cpp", "test_shim.cpp")
+    hdr = os.path.join(ROOT, "qsfs-fuse_amd", "host", "qsfs_md5.hpp")
+    if not os.path.exists(BIN) or os.path.getmtime(BIN) < max(os.path.getmtime(src), os.path.getmtime(hdr)):
+        build_shim()
+    return BIN
+
+
+@pytest.mark.gpu
+def test_cpp_dropin_shim():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    check_shim_output(subprocess.run([shim_binary()], capture_output=True, text=True, timeout=300))
+
+
+def test_cpp_dropin_shim_cpu_backend():
+    """The same drop-in program with the library's CPU backend (QSMD5_BACKEND=cpu,
+    no GPU needed): the C++ surface, the stream side effects and the class's
+    copy semantics hold whichever backend hashes."""
+    env = dict(os.environ, QSMD5_BACKEND="cpu")
+    check_shim_output(subprocess.run([shim_binary()], capture_output=True, text=True, timeout=300, env=env))
