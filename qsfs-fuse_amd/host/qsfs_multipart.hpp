@@ -28,7 +28,12 @@
 //   - with `pipeline` (default), the next wave is gathered and hashed on a
 //     helper thread while this thread uploads the current one, so the hash
 //     time hides behind the upload (the overlap the reference's async
-//     handler has, QSTransferManager.cpp:654-659).
+//     handler has, QSTransferManager.cpp:654-659);
+//   - the transfer's cancel flag (opt.should_continue, the reference's
+//     handle->ShouldContinue() at QSTransferManager.cpp:608 and 646) is asked
+//     before a wave takes buffers and before each part's upload; a cancelled
+//     upload returns every buffer it did not hand over and reports how many
+//     parts it uploaded, so the caller marks the rest failed (:669-671).
 //
 // The pool holds `-n` (numtransfer) buffers of `-b` MiB: the transfer
 // manager's heap is bufSize x maxParallelTransfers (TransferManager.h:74-86,
@@ -49,6 +54,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <exception>
+#include <functional>
 #include <future>
 #include <mutex>
 #include <stdexcept>
@@ -170,6 +176,8 @@ class BlockingPool {
 // waiting for the next wave to be ready, i.e. hashing NOT hidden.
 struct WaveStats {
   size_t waves = 0, parts = 0;
+  size_t uploaded = 0;   // parts handed to upload(), in part order: parts[0, uploaded)
+  bool stopped = false;  // should_continue() said stop (TransferHandle::ShouldContinue)
   size_t gpu_waves = 0, cpu_waves = 0, split_waves = 0;  // by qsmd5_last_backend of each wave
   size_t widest_wave = 0;
   double gather_s = 0, hash_s = 0, upload_s = 0, wait_s = 0, wall_s = 0;
@@ -181,6 +189,13 @@ struct PrehashOptions {
   bool upload_releases = false;  // true: a buffer is upload()'s once upload() returns, and
                                  // its completion handler releases it (an async
                                  // executor); false: released when upload() returns
+  // The transfer's cancel flag (TransferHandle::ShouldContinue, TransferHandle.h:159-162),
+  // asked where the reference's loop asks it (QSTransferManager.cpp:608, 646): before a
+  // wave takes buffers and before each part is handed to upload().  Once it says
+  // false, no further part is uploaded, every buffer not handed over goes back
+  // to the pool, and the call returns with stats.stopped; the caller marks
+  // parts [stats.uploaded, end) failed, as :669-671.  Empty: never stop.
+  std::function<bool()> should_continue;
 };
 
 namespace detail {
@@ -188,6 +203,7 @@ namespace detail {
 template <class Pool>
 struct Wave {
   size_t first = 0;  // index of its first part
+  bool cancelled = false;  // should_continue() was false before it took a buffer
   std::vector<typename Pool::buffer_type> bufs;
   std::vector<uint8_t> dig;
   int backend = 0;
@@ -209,10 +225,14 @@ void release_all(Pool& pool, std::vector<typename Pool::buffer_type>& bufs, size
 // buffers then alternate between the wave in upload and the wave in hashing.
 template <class Pool, class Read>
 Wave<Pool> prepare_wave(const std::vector<qsmd5_part>& parts, size_t first, Pool& pool, Read& read,
-                        size_t max_wave, bool keep_half) {
+                        size_t max_wave, bool keep_half, const std::function<bool()>& should_continue) {
   using clock = std::chrono::steady_clock;
   Wave<Pool> w;
   w.first = first;
+  if (should_continue && !should_continue()) {
+    w.cancelled = true;
+    return w;
+  }
   const size_t want = std::min(max_wave ? max_wave : parts.size(), parts.size() - first);
   typename Pool::buffer_type b = pool.acquire();
   if (!Pool::data(b)) throw std::runtime_error("transfer buffer pool is shut down: upload stopped");
@@ -272,7 +292,8 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
     return std::chrono::duration<double>(b - a).count();
   };
   auto prep = [&](size_t first) {
-    return detail::prepare_wave(parts, first, pool, read, opt.max_wave, opt.pipeline && first == 0);
+    return detail::prepare_wave(parts, first, pool, read, opt.max_wave, opt.pipeline && first == 0,
+                                opt.should_continue);
   };
   std::future<W> ahead;  // the next wave, being prepared on the helper thread
   // On the way out after a failure: the wave in preparation finishes (its
@@ -286,8 +307,13 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
     } catch (...) {
     }
   };
+  auto stop_requested = [&] { return opt.should_continue && !opt.should_continue(); };
   W cur = prep(0);
   for (;;) {
+    if (cur.cancelled) {  // stopped before this wave took a buffer; nothing is ahead of it
+      st.stopped = true;
+      break;
+    }
     const size_t n = cur.bufs.size(), next = cur.first + n;
     ++st.waves;
     st.parts += n;
@@ -310,6 +336,7 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
     size_t k = 0;
     try {
       for (; k < n; ++k) {
+        if (stop_requested()) break;
         const qsmd5_part& p = parts[cur.first + k];
         const std::string hex = detail::hex(&cur.dig[16 * k]);
         // A buffer is upload()'s once upload() returns (upload_releases: its
@@ -324,6 +351,7 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
         }
         if (!opt.upload_releases) pool.release(cur.bufs[k]);  // ReceivedHandlerMultipleUpload
         cur.bufs[k] = typename Pool::buffer_type();
+        ++st.uploaded;
       }
     } catch (...) {
       detail::release_all(pool, cur.bufs, k + 1);  // parts of this wave never handed over
@@ -332,6 +360,12 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
     }
     const auto t1 = clock::now();
     st.upload_s += secs(t0, t1);
+    if (k < n) {  // stopped inside the wave: the rest of it and the wave ahead go back
+      detail::release_all(pool, cur.bufs, k);
+      drain_ahead();
+      st.stopped = true;
+      break;
+    }
     if (next >= parts.size()) break;
     if (ahead.valid()) {
       cur = ahead.get();  // rethrows the helper's failure (its buffers are already back)

@@ -29,6 +29,7 @@
 // is one LCG(seed + f) stream.  Prints one JSON object with the digests in
 // part order and where the time went; tests/test_gpu_multipart.py and
 // tests/test_multipart_cpu.py check the digests.
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -314,6 +315,7 @@ int main(int argc, char** argv) {
   int repeat = 1, async_threads = 0;
   double upload_ms = 0, deadlock_s = 20;
   uint32_t short_read_part = 0, fail_upload_part = 0;  // fault injection (1-based part numbers)
+  size_t cancel_after = SIZE_MAX;  // each file's transfer is cancelled once it handed this many parts on
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&](const char* key) { return a.rfind(key, 0) == 0 ? a.c_str() + strlen(key) : nullptr; };
@@ -330,6 +332,7 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--deadlock-s=")) deadlock_s = atof(v);
     else if (const char* v = val("--short-read-part=")) short_read_part = (uint32_t)strtoul(v, nullptr, 0);
     else if (const char* v = val("--fail-upload-part=")) fail_upload_part = (uint32_t)strtoul(v, nullptr, 0);
+    else if (const char* v = val("--cancel-after=")) cancel_after = strtoull(v, nullptr, 0);
     else if (a == "--aligned") aligned = true;
     else if (a == "--pinned") pinned = true;
     else if (a == "--slab") slab = true;
@@ -441,6 +444,9 @@ int main(int argc, char** argv) {
           opt.pipeline = pipeline;
           opt.max_wave = max_wave;
           opt.upload_releases = exec != nullptr;
+          // --cancel-after: TransferHandle::Cancel from another thread once K parts went out
+          std::atomic<size_t> handed{0};
+          if (cancel_after != SIZE_MAX) opt.should_continue = [&] { return handed.load() < cancel_after; };
           InFlight inflight;
           auto read = [&](const qsmd5_part& p, char* dst) {
             const size_t got = pf.read(p.offset, p.size, dst);
@@ -448,6 +454,7 @@ int main(int argc, char** argv) {
           };
           auto upload = [&](const qsmd5_part& p, const qsmd5::PoolBuffer& b, const std::string& hex) {
             if (p.part_number == fail_upload_part) throw std::runtime_error("injected upload failure");
+            ++handed;
             if (!exec) {  // sync: UploadMultipart on this thread, the buffer released after it
               sleep_ms(upload_ms);
               md5[f][p.part_number - 1] = hex;
@@ -464,6 +471,7 @@ int main(int argc, char** argv) {
           };
           st[f] = qsmd5::upload_parts_prehashed(parts, shared, read, upload, opt);
           inflight.wait();
+          if (st[f].uploaded != handed.load()) errors[f] = "stats.uploaded disagrees with the parts uploaded";
         } catch (const std::exception& e) {
           errors[f] = e.what();
         }
@@ -499,7 +507,10 @@ int main(int argc, char** argv) {
       for (auto& b : pool) qsmd5_unregister_host(b.data);
   }
   qsmd5::WaveStats sum;
+  size_t stopped = 0;
   for (const auto& s : st) {
+    stopped += s.stopped;
+    sum.uploaded += s.uploaded;
     sum.waves += s.waves;
     sum.parts += s.parts;
     sum.gpu_waves += s.gpu_waves;
@@ -516,13 +527,13 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < v.size(); ++i) s += std::string(i ? ", " : "") + "\"" + v[i] + "\"";
     return s + "]";
   };
-  printf("{\"deadlock\": false, \"error\": \"%s\", \"uploaded\": %zu, \"pool_free_after\": %zu, \"size\": %llu, \"parts\": %zu, \"files\": %zu, \"pages\": %zu, \"pool\": %zu, "
+  printf("{\"deadlock\": false, \"error\": \"%s\", \"uploaded\": %zu, \"stats_uploaded\": %zu, \"stopped\": %zu, \"pool_free_after\": %zu, \"size\": %llu, \"parts\": %zu, \"files\": %zu, \"pages\": %zu, \"pool\": %zu, "
          "\"pinned\": %s, \"slab\": %s, \"registered\": %s, \"pipeline\": %s, \"async_threads\": %d, "
          "\"naive_wave\": %zu, \"upload_ms\": %.3f, \"register_s\": %.6f, \"waves\": %zu, "
          "\"widest_wave\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"split_waves\": %zu, "
          "\"seconds\": %.6f, \"gather_s\": %.6f, \"hash_s\": %.6f, \"upload_s\": %.6f, \"wait_s\": %.6f, "
          "\"part_sizes\": [",
-         errors[0].c_str(), uploaded, pool_free_after, (unsigned long long)size, n, files, file[0].pages.size(), pool_n, pinned ? "true" : "false",
+         errors[0].c_str(), uploaded, sum.uploaded, stopped, pool_free_after, (unsigned long long)size, n, files, file[0].pages.size(), pool_n, pinned ? "true" : "false",
          slab ? "true" : "false", reg && !pinned ? "true" : "false", pipeline ? "true" : "false",
          async_threads, naive_wave, upload_ms, register_s, sum.waves, sum.widest_wave, sum.gpu_waves,
          sum.cpu_waves, sum.split_waves, total, sum.gather_s, sum.hash_s, sum.upload_s, sum.wait_s);

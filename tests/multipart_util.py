@@ -9,9 +9,18 @@ from conftest import ROOT
 HARNESS = os.path.join(ROOT, "tests", "cpp", "multipart_harness")
 
 
+def newest_source():
+    """The harness is rebuilt when it or any header it compiles in changed."""
+    paths = [os.path.join(ROOT, "tests", "cpp", "multipart_harness.cpp"),
+             os.path.join(ROOT, "qsfs-fuse_amd", "host", "qsfs_multipart.hpp"),
+             os.path.join(ROOT, "qsfs-fuse_amd", "host", "qsfs_md5.hpp"),
+             os.path.join(ROOT, "include", "qsmd5.h")]
+    return max(os.path.getmtime(p) for p in paths)
+
+
 def build():
     src = os.path.join(ROOT, "tests", "cpp", "multipart_harness.cpp")
-    if not os.path.exists(HARNESS) or os.path.getmtime(HARNESS) < os.path.getmtime(src):
+    if not os.path.exists(HARNESS) or os.path.getmtime(HARNESS) < newest_source():
         subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", src,
                                "-I" + os.path.join(ROOT, "include"),
                                "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
@@ -42,9 +51,7 @@ def build_tsan():
     pool, executor handoff) under ThreadSanitizer; libqsmd5 itself is not
     instrumented (its own threads are covered by test_gpu_sanitizers.py)."""
     src = os.path.join(ROOT, "tests", "cpp", "multipart_harness.cpp")
-    hdr = os.path.join(ROOT, "qsfs-fuse_amd", "host", "qsfs_multipart.hpp")
-    newest = max(os.path.getmtime(src), os.path.getmtime(hdr))
-    if not os.path.exists(HARNESS_TSAN) or os.path.getmtime(HARNESS_TSAN) < newest:
+    if not os.path.exists(HARNESS_TSAN) or os.path.getmtime(HARNESS_TSAN) < newest_source():
         subprocess.check_call(["/opt/rocm/llvm/bin/clang++", "-std=c++17", "-O1", "-g",
                                "-fsanitize=thread", src, "-I" + os.path.join(ROOT, "include"),
                                "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",

@@ -99,8 +99,9 @@ def test_pipeline_hides_hashing_behind_upload():
     assert piped["seconds"] < serial["seconds"]
 
 
-@pytest.mark.parametrize("mode", [[], ["--async=3"], ["--no-pipeline"], ["--max-wave=2"]],
-                         ids=["sync", "async", "no_pipeline", "max_wave_2"])
+@pytest.mark.parametrize("mode", [[], ["--async=3"], ["--no-pipeline"], ["--max-wave=2"],
+                                  ["--cancel-after=5"], ["--cancel-after=5", "--async=3"]],
+                         ids=["sync", "async", "no_pipeline", "max_wave_2", "cancel", "cancel_async"])
 def test_concurrent_files_under_tsan(mode):
     """The drop-in header's threads -- the pipeline's helper thread preparing
     the next wave, the shared pool, the executor's completion handler
@@ -115,7 +116,9 @@ def test_concurrent_files_under_tsan(mode):
     assert "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-8000:]
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads(out.stdout)
-    assert r["deadlock"] is False and all(m == gold[:12] for m in r["md5_files"])
+    want = 5 if "--cancel-after=5" in mode else 12
+    assert r["deadlock"] is False and r["pool_free_after"] == 5, r
+    assert all(m[:want] == gold[:want] and not any(m[want:]) for m in r["md5_files"]), r["md5_files"]
 
 
 @pytest.mark.parametrize("fault,mode,want_uploaded", [
@@ -147,3 +150,31 @@ def test_failures_stop_the_upload_and_return_every_buffer(fault, mode, want_uplo
     assert [r["md5"][i] for i in done] == gold[:len(done)]
     if want_uploaded is not None:
         assert r["uploaded"] == want_uploaded, r
+
+
+@pytest.mark.parametrize("after,mode", [(0, []), (1, []), (7, []), (7, ["--no-pipeline"]), (7, ["--async=2"]),
+                                        (3, ["--files=3"]), (19, []), (20, [])],
+                         ids=["before_first", "after_1", "after_7", "after_7_no_pipeline", "after_7_async",
+                              "three_files", "after_19", "after_all"])
+def test_cancel_stops_the_upload_and_returns_every_buffer(after, mode):
+    """The transfer's cancel flag (TransferHandle::ShouldContinue, asked by
+    the reference before each part, QSTransferManager.cpp:608 and 646): once
+    it says stop, no further part is handed to the upload, the call returns
+    normally with stats.stopped and stats.uploaded == the parts handed on
+    (the caller marks the rest failed, :669-671), and every buffer -- the
+    wave's, the one the helper thread was preparing -- is back in the pool."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    args = ["--aligned", "--size=%d" % (20 * 10 * MiB), "--pool=4", "--upload-ms=1",
+            "--cancel-after=%d" % after] + mode
+    out = run_raw(args, "cpu", timeout=120)
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads(out.stdout)
+    files = r["files"]
+    assert r["error"] == "" and r["deadlock"] is False, r
+    assert r["pool_free_after"] == 4, r
+    want = min(after, 20)
+    assert r["stats_uploaded"] == want * files and r["uploaded"] == want * files, r
+    # the last part handed on ends the loop before anyone asks again
+    assert r["stopped"] == (files if after < 20 else 0), r
+    for m in r["md5_files"]:
+        assert m[:want] == gold[:want] and not any(m[want:]), m
