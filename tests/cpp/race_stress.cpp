@@ -18,9 +18,14 @@
 // Every digest is checked against the CPU oracle (oracle/md5_oracle.c, the
 // checker, linked only into this test).
 // usage: race_stress [threads=6] [rounds=12] [max_len=3145728] [racy]
+// Without a GPU it runs only with QSMD5_BACKEND=cpu (the library's CPU
+// backend: its worker threads and multi-buffer lanes, under the same
+// sanitizers, in the container's `not gpu` suite); pinned buffers are then
+// refused with -ENODEV and the case hashes a heap copy instead.
 // `racy` adds a deliberate unsynchronised counter shared by the threads: the
 // negative control showing that the TSan build, with its HIP suppressions,
 // still reports a race in instrumented code.
+#include <errno.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -47,6 +52,7 @@ namespace {
 std::atomic<int> g_bad{0};
 std::atomic<long> g_checked{0};
 bool g_racy = false;
+bool g_cpu_only = false;  // no GPU, QSMD5_BACKEND=cpu
 long g_racy_counter = 0;  // written without a lock when g_racy (negative control)
 
 void check(const uint8_t* p, uint64_t len, const uint8_t got[16], const char* what, int t, int r) {
@@ -101,6 +107,7 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
   while (ready->load() < nthreads) {
   }
   int rc = qsmd5_init(0);
+  if (rc == -ENODEV && g_cpu_only) rc = 0;  // no GPU to bind: the calls hash on the CPU
   if (rc != 0) {
     fail("init", rc, t, -1);
     return;
@@ -142,10 +149,17 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
           break;
         }
         const size_t len = next(s) % (max_len / 2) + 1;
+        const size_t fork_at = next(s) % len;  // a copy of the context taken here (MD5 is a value type)
+        qsmd5_ctx* copy = nullptr;
         size_t at = 0;
         while (at < len && rc == 0) {
           size_t piece = next(s) % (len / 3 + 70) + 1;
           if (piece > len - at) piece = len - at;
+          if (!copy && at + piece > fork_at) piece = fork_at - at;
+          if (!copy && at == fork_at) {
+            if ((rc = qsmd5_ctx_copy(c, &copy)) != 0) break;
+            continue;
+          }
           rc = qsmd5_ctx_update(c, buf.data() + at, piece);
           at += piece;
         }
@@ -153,13 +167,26 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
         qsmd5_ctx_destroy(c);
         if (rc != 0) fail("ctx", rc, t, r);
         else check(buf.data(), len, d, "ctx", t, r);
+        if (copy && rc == 0) {  // the copy hashes the rest in one piece, by itself
+          uint8_t dc[16];
+          if ((rc = qsmd5_ctx_update(copy, buf.data() + fork_at, len - fork_at)) == 0) rc = qsmd5_ctx_final(copy, dc);
+          if (rc != 0) fail("ctx copy", rc, t, r);
+          else check(buf.data(), len, dc, "ctx copy", t, r);
+        }
+        qsmd5_ctx_destroy(copy);
         break;
       }
       case 3: {  // pinned buffer from the pool API
         const size_t len = next(s) % (max_len / 2) + 1;
         void* p = nullptr;
         if ((rc = qsmd5_alloc_pinned(len, &p)) != 0) {
-          fail("alloc_pinned", rc, t, r);
+          if (rc != -ENODEV || !g_cpu_only) {
+            fail("alloc_pinned", rc, t, r);
+            break;
+          }
+          std::vector<uint8_t> heap(buf.begin() + 7, buf.begin() + 7 + len);  // no GPU: a heap copy
+          if ((rc = qsmd5_hash_one(heap.data(), len, d)) != 0) fail("hash_one(heap)", rc, t, r);
+          else check(heap.data(), len, d, "hash_one(heap)", t, r);
           break;
         }
         memcpy(p, buf.data() + 7, len);
@@ -213,8 +240,12 @@ int main(int argc, char** argv) {
   }
   g_racy = argc > 4 && strcmp(argv[4], "racy") == 0;
   if (qsmd5_device_count() < 1) {
-    fprintf(stderr, "no GPU\n");
-    return 2;
+    const char* be = getenv("QSMD5_BACKEND");
+    if (!be || strcmp(be, "cpu") != 0) {
+      fprintf(stderr, "no GPU\n");
+      return 2;
+    }
+    g_cpu_only = true;
   }
   std::atomic<int> ready{0};
   std::vector<std::thread> th;

@@ -25,3 +25,35 @@ def test_sanitized_binary_starts(variant):
         assert "no GPU" in text, text
     else:  # a GPU is visible: the short stress must then pass
         assert out.returncode == 0 and "race_stress ok" in out.stdout, text[-3000:]
+
+
+@pytest.mark.parametrize("groups", ["1", "2"], ids=["16_lanes", "32_lanes"])
+@pytest.mark.parametrize("variant", ["tsan", "asan"])
+def test_race_stress_cpu_backend(variant, groups):
+    """The same stress with the library's CPU backend and no GPU
+    (QSMD5_BACKEND=cpu): six threads racing every entry point -- hash_one,
+    ragged batches over the backend's worker threads and 16- or 32-lane
+    multi-buffer cores, streaming contexts copied mid-stream, shutdown and
+    re-init -- under ThreadSanitizer, and under AddressSanitizer + UBSan.
+    Every digest is checked against the oracle inside the binary."""
+    exe = os.path.join(SAN, "race_stress_" + variant)
+    env = dict(os.environ, QSMD5_BACKEND="cpu", QSMD5_CPU_THREADS="4", QSMD5_CPU_MB_GROUPS=groups,
+               ASAN_OPTIONS="detect_leaks=0", TSAN_OPTIONS="halt_on_error=0:exitcode=66")
+    out = subprocess.run(["setarch", "x86_64", "-R", exe, "6", "16"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    text = out.stdout + out.stderr
+    if out.returncode == 2 and "no GPU" in text:
+        pytest.skip("binary predates the CPU mode")
+    assert "Sanitizer" not in text and "runtime error" not in text, text[-4000:]
+    assert out.returncode == 0 and "race_stress ok" in out.stdout, text[-3000:]
+
+
+def test_tsan_negative_control_cpu_backend():
+    """The planted unsynchronised counter is reported by the TSan build on the
+    CPU backend too: the check above would see a race."""
+    exe = os.path.join(SAN, "race_stress_tsan")
+    env = dict(os.environ, QSMD5_BACKEND="cpu", TSAN_OPTIONS="halt_on_error=0:exitcode=66")
+    out = subprocess.run(["setarch", "x86_64", "-R", exe, "4", "4", "65536", "racy"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert "WARNING: ThreadSanitizer: data race" in out.stderr, (out.stdout + out.stderr)[-3000:]
+    assert out.returncode == 66
