@@ -10,13 +10,17 @@ import pytest
 from conftest import ROOT
 
 SAN = os.path.join(ROOT, "qsfs-fuse_amd", "lib", "san")
+# The same suppressions as tests/test_gpu_sanitizers.py: on a machine with a
+# GPU even QSMD5_BACKEND=cpu starts the uninstrumented HIP/HSA runtimes
+# (qsmd5_device_count), whose own threads TSan would otherwise report.
+TSAN = ("halt_on_error=0:exitcode=66:suppressions=" + os.path.join(ROOT, "tests", "cpp", "tsan_hip.supp"))
 
 
 @pytest.mark.parametrize("variant", ["tsan", "asan"])
 def test_sanitized_binary_starts(variant):
     exe = os.path.join(SAN, "race_stress_" + variant)
     assert os.path.exists(exe), "run __graft_entry__.build() (scripts/build_sanitized.sh)"
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", TSAN_OPTIONS="exitcode=66")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0", TSAN_OPTIONS=TSAN)
     out = subprocess.run([exe, "2", "1", "4096"], env=env, capture_output=True, text=True,
                          timeout=120)
     text = out.stdout + out.stderr
@@ -38,7 +42,7 @@ def test_race_stress_cpu_backend(variant, groups):
     Every digest is checked against the oracle inside the binary."""
     exe = os.path.join(SAN, "race_stress_" + variant)
     env = dict(os.environ, QSMD5_BACKEND="cpu", QSMD5_CPU_THREADS="4", QSMD5_CPU_MB_GROUPS=groups,
-               ASAN_OPTIONS="detect_leaks=0", TSAN_OPTIONS="halt_on_error=0:exitcode=66")
+               ASAN_OPTIONS="detect_leaks=0", TSAN_OPTIONS=TSAN)
     out = subprocess.run(["setarch", "x86_64", "-R", exe, "6", "16"], env=env,
                          capture_output=True, text=True, timeout=300)
     text = out.stdout + out.stderr
@@ -52,7 +56,7 @@ def test_tsan_negative_control_cpu_backend():
     """The planted unsynchronised counter is reported by the TSan build on the
     CPU backend too: the check above would see a race."""
     exe = os.path.join(SAN, "race_stress_tsan")
-    env = dict(os.environ, QSMD5_BACKEND="cpu", TSAN_OPTIONS="halt_on_error=0:exitcode=66")
+    env = dict(os.environ, QSMD5_BACKEND="cpu", TSAN_OPTIONS=TSAN)
     out = subprocess.run(["setarch", "x86_64", "-R", exe, "4", "4", "65536", "racy"], env=env,
                          capture_output=True, text=True, timeout=300)
     assert "WARNING: ThreadSanitizer: data race" in out.stderr, (out.stdout + out.stderr)[-3000:]
