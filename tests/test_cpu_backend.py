@@ -259,6 +259,9 @@ def test_split_routing_rule(monkeypatch):
 def test_split_batch_digests_on_cpu_only_box(monkeypatch):
     """Without a GPU a split batch still returns every digest (its GPU share
     falls back to the CPU) and matches the oracle chunk by chunk."""
+    if qsmd5.device_count() > 0:
+        pytest.skip("a GPU is visible: routing prices this host's measured rates and the "
+                    "batch need not split (the GPU suite covers split batches)")
     monkeypatch.setenv("QSMD5_BACKEND", "auto")
     monkeypatch.setenv("QSMD5_CPU_THREADS", "1")  # a small batch that still favours the GPU
     monkeypatch.delenv("QSMD5_SPLIT", raising=False)
@@ -382,7 +385,12 @@ def test_lane_priced_routing_is_opt_in(monkeypatch, golden):
     monkeypatch.setenv("QSMD5_ROUTE_LANES", "1")
     assert qsmd5.route(lens) == C
     assert qsmd5.route([10 * MiB] * 64) == C
+    # 512 x 10 MiB is a GPU batch for one CPU thread's lanes on any host; at 4
+    # threads a fast AVX-512 host's lanes can outrun the link (the MI355X box's
+    # EPYC does, 5 GiB at ~37 GiB/s), which the router then rightly prices
+    monkeypatch.setenv("QSMD5_CPU_THREADS", "1")
     assert qsmd5.route([10 * MiB] * 512) == G
+    monkeypatch.setenv("QSMD5_CPU_THREADS", "4")
     assert qsmd5.route([10 * MiB]) == C  # a lone part: scalar, as before
     monkeypatch.setenv("QSMD5_CPU_MB", "0")  # no lanes, nothing to price
     assert qsmd5.route(lens) == S
