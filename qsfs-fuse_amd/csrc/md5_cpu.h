@@ -40,7 +40,7 @@ void md5_mb16(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[1
               void* ctx);
 // The same with 32 lanes: two 16-lane groups whose chains interleave, for
 // cores with the vector pipes to run both (the runtime times both once and
-// keeps the faster, qsmd5_runtime.cpp measure_cpu_rates).
+// keeps the faster, qsmd5_rt_route.cpp measure_cpu_rates).
 void md5_mb32(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16], MbPull pull,
               void* ctx);
 

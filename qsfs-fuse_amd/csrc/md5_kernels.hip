@@ -17,7 +17,7 @@
 //                            per-lane loads, 5 VALU per step.
 //   qsmd5_column_pc[2]_kernel  the latency kernels over one column of a
 //                            host-staged batch: chains resume from and park in
-//                            HBM state (qsmd5_runtime.cpp run_batch).
+//                            HBM state (qsmd5_rt_staging.cpp run_batch).
 // Streaming (the MD5 class, MD5.cpp:240-312): update() runs its blocks as a
 // one-lane qsmd5_column_pc_kernel batch; then
 //   qsmd5_final_kernel       tail + padding + length (finalize()).
@@ -408,7 +408,7 @@ extern "C" __global__ __launch_bounds__(256) void qsmd5_lcg_fill_kernel(
 // chunks): see the producer/consumer notes at kPcHalf.
 //
 // kColumn = false: chunks[order[t]] is a whole chunk; digest -> digests[idx].
-// kColumn = true (column-pipelined host batches, qsmd5_runtime.cpp): the batch
+// kColumn = true (column-pipelined host batches, qsmd5_rt_staging.cpp): the batch
 // is cut into columns [col_off, col_off + col_w) of every chunk.  chunks[t] is
 // lane t's staged SEGMENT {ptr = segment start, len = the chunk's TOTAL
 // length L} and idx = order[t] names the chunk.  A lane resumes from
@@ -429,7 +429,7 @@ extern "C" __global__ __launch_bounds__(256) void qsmd5_lcg_fill_kernel(
 constexpr uint32_t kSkewMinBlocks = 1u << 19;
 //
 // kNT: the producer's loads carry the non-temporal cache policy (chosen per
-// launch by the host, qsmd5_runtime.cpp load_nt_for).
+// launch by the host, qsmd5_rt_staging.cpp load_nt_for).
 // kTrace (ubench only): the chain wave's lane 0 stamps s_memtime and
 // s_memrealtime every 4096 phases into trace[workgroup][2 * (p / 4096) + {0,1}],
 // and at the end the cycles each wave spent: trace[workgroup][1019] producer
@@ -879,7 +879,7 @@ extern "C" __global__ __launch_bounds__(64) void qsmd5_batch_coal_kernel(
 #undef QS_LP
 
 // ---------------------------------------------------------------------------
-// Gather of host rows into the staging ring (qsmd5_runtime.cpp run_batch).
+// Gather of host rows into the staging ring (qsmd5_rt_staging.cpp run_batch).
 // Rows that cannot share a 2-D DMA copy -- pinned buffers in separate
 // allocations, each one HIP allocation on its own -- would otherwise cost one
 // hipMemcpyAsync each (~8-10 us of overhead per 256 KiB column row).  Pinned

@@ -1,6 +1,6 @@
 // qsfs-fuse_amd/csrc/qsmd5_plan.h -- the staging plan for host-resident chunks.
 //
-// Pure host logic (no HIP), shared by the runtime (qsmd5_runtime.cpp run_batch)
+// Pure host logic (no HIP), shared by the runtime (qsmd5_rt_staging.cpp run_batch)
 // and the CPU tests (tests/cpp/test_plan.cpp), which check its invariants.
 //
 // Host-resident chunks (the qsfs case: parts in pooled host buffers,
@@ -157,7 +157,7 @@ inline HostPlan plan_host(const std::vector<uint64_t>& host_len, uint64_t stagin
   return P;
 }
 
-// H2D copy runs of one slice (qsmd5_runtime.cpp run_batch).  Rows k .. k+rows-1
+// H2D copy runs of one slice (qsmd5_rt_staging.cpp run_batch).  Rows k .. k+rows-1
 // of a slice's active chunks go as ONE hipMemcpy2DAsync when they have equal
 // widths, a constant source stride >= the width (and < 2^40), AND their whole
 // source span [src(k), src(k + rows - 1) + w) lies inside one allocation or
@@ -209,7 +209,7 @@ inline std::vector<CopyRun> plan_copy_runs(size_t n, Src&& src, Width&& w, SpanO
   return runs;
 }
 
-// Multi-GPU split of host chunks (qsmd5_runtime.cpp run_sharded).  North star:
+// Multi-GPU split of host chunks (qsmd5_rt_staging.cpp run_sharded).  North star:
 // shard "only when one file's part count exceeds a single GPU's batch"; and
 // host data is bound by each GPU's own PCIe link, so large host batches gain
 // from more links.  The chunks (in caller order, lengths host_len) go in
@@ -242,7 +242,7 @@ inline std::vector<uint32_t> plan_shards(const std::vector<uint64_t>& host_len, 
   return shard;
 }
 
-// The host-ordered staging schedule (qsmd5_runtime.cpp run_batch): S slices,
+// The host-ordered staging schedule (qsmd5_rt_staging.cpp run_batch): S slices,
 // nregions ring regions (slice si fills region si % nregions), the copies of
 // slice si enqueued at most after the host has seen the kernel of slice
 // si - nregions finish (its region is then free), the kernel of slice si

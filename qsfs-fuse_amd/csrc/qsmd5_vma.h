@@ -1,7 +1,7 @@
 // qsfs-fuse_amd/csrc/qsmd5_vma.h -- which VMAs may be cached as host memory.
 //
 // Pure host logic, shared by the runtime's pointer classifier
-// (qsmd5_runtime.cpp Classifier) and the CPU test tests/cpp/test_vma.cpp.
+// (qsmd5_rt.h Classifier) and the CPU test tests/cpp/test_vma.cpp.
 //
 // A pointer HIP does not know (pageable memory) is remembered by the VMA that
 // holds it, so later chunks in that VMA skip the per-pointer query.  A VMA

@@ -24,13 +24,17 @@ for v in tsan asan; do
   esac
   HOSTSAN=""
   for f in $SAN; do HOSTSAN="$HOSTSAN -Xarch_host $f"; done
-  $HIPCC -O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $HOSTSAN \
-    -x hip -c "$R/qsfs-fuse_amd/csrc/qsmd5_runtime.cpp" -o "$OUT/qsmd5_runtime_$v.o"
+  RT_OBJS=""
+  for u in qsmd5_runtime qsmd5_rt_device qsmd5_rt_staging qsmd5_rt_route; do
+    $HIPCC -O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $HOSTSAN \
+      -x hip -c "$R/qsfs-fuse_amd/csrc/$u.cpp" -o "$OUT/${u}_$v.o"
+    RT_OBJS="$RT_OBJS $OUT/${u}_$v.o"
+  done
   $CXX -O1 -g -std=c++17 -fPIC $SAN -c "$R/qsfs-fuse_amd/csrc/md5_cpu.cpp" -o "$OUT/md5_cpu_$v.o"
   $CXX -O1 -g -std=c++17 -fPIC $SAN -c "$R/qsfs-fuse_amd/csrc/md5_cpu_mb.cpp" -o "$OUT/md5_cpu_mb_$v.o"
   $CXX -O1 -g -std=c++17 $SAN -c "$R/tests/cpp/race_stress.cpp" -o "$OUT/race_stress_$v.o"
   $CC -O1 -g -std=c11 $SAN -c "$R/oracle/md5_oracle.c" -o "$OUT/md5_oracle_$v.o"
-  $CXX $SAN -o "$OUT/race_stress_$v" "$OUT/race_stress_$v.o" "$OUT/qsmd5_runtime_$v.o" "$OUT/md5_cpu_$v.o" "$OUT/md5_cpu_mb_$v.o" \
+  $CXX $SAN -o "$OUT/race_stress_$v" "$OUT/race_stress_$v.o" $RT_OBJS "$OUT/md5_cpu_$v.o" "$OUT/md5_cpu_mb_$v.o" \
     "$R/qsfs-fuse_amd/lib/md5_kernels.o" "$OUT/md5_oracle_$v.o" \
     -L/opt/rocm/lib -lamdhip64 -lpthread -Wl,-rpath,/opt/rocm/lib
 done

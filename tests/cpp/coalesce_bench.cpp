@@ -1,5 +1,5 @@
 // tests/cpp/coalesce_bench.cpp -- native callers of the group commit
-// (qsmd5_runtime.cpp): T threads each hash one P-byte part R times in a tight
+// (qsmd5_rt_route.cpp): T threads each hash one P-byte part R times in a tight
 // loop, as qsfs's numtransfer executor threads call md5() part after part
 // (TransferManager.cpp:55-60, QSClient.cpp:370).  Prints one JSON line with
 // the wall time and whether every digest matched the first round's.

@@ -1,5 +1,5 @@
 // tests/cpp/test_plan.cpp -- CPU checks of the host-staging plan
-// (qsfs-fuse_amd/csrc/qsmd5_plan.h, used by qsmd5_runtime.cpp run_batch).
+// (qsfs-fuse_amd/csrc/qsmd5_plan.h, used by qsmd5_rt_staging.cpp run_batch).
 //
 // For many length mixes (qsfs part sets, ragged, tiny, one huge chunk), ring
 // sizes, slice targets and column widths, the plan must:

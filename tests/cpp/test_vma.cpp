@@ -1,6 +1,6 @@
 // tests/cpp/test_vma.cpp -- CPU checks of qsfs-fuse_amd/csrc/qsmd5_vma.h, the
 // rule for which /proc/self/maps VMAs the runtime's pointer classifier may
-// remember as host memory (qsmd5_runtime.cpp Classifier).
+// remember as host memory (qsmd5_rt.h Classifier).
 //   1. readable anonymous, [heap], [stack], [anon:...] and regular-file VMAs
 //      qualify, with their exact [lo, hi);
 //   2. unreadable reservations (---p: where VRAM is mapped), /dev files

@@ -173,7 +173,7 @@ def test_routing_rule(monkeypatch):
 
 def _predicted_break_even(r, S):
     """First n for which equal host parts of S bytes go to the GPU, by the cost
-    model of qsmd5_runtime.cpp ("backend routing") at rates r."""
+    model of qsmd5_rt_route.cpp ("backend routing") at rates r."""
     GiB = float(1 << 30)
     T, rc, g, K = r["cpu_threads"], r["cpu_chain_gibs"], r["gpu_chain_gibs"], r["link_gibs"]
     for n in range(1, 1 << 16):

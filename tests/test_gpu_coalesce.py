@@ -1,4 +1,4 @@
-"""Group commit of concurrent qsmd5_hash_batch calls (qsmd5_runtime.cpp).
+"""Group commit of concurrent qsmd5_hash_batch calls (qsmd5_rt_route.cpp).
 
 qsfs calls md5() from up to numtransfer worker threads at once
 (TransferManager.cpp:55-60), each call one part.  A launch costs one chain

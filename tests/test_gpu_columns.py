@@ -1,4 +1,4 @@
-"""Column-pipelined staging of host-resident batches (qsmd5_runtime.cpp run_batch,
+"""Column-pipelined staging of host-resident batches (qsmd5_rt_staging.cpp run_batch,
 qsmd5_column_pc_kernel) on an MI355X.
 
 A host batch is cut into columns of W bytes per chunk; each column is one H2D

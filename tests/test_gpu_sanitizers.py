@@ -10,7 +10,7 @@ pool from several threads and checks every digest against the oracle.  A
 sanitizer report fails the test even when every digest matched.
 
 QSMD5_DEVICES=0,0 binds two contexts to the box's one GPU, so the batch
-splitter's per-device threads (qsmd5_runtime.cpp, in-process sharding) run
+splitter's per-device threads (qsmd5_rt_staging.cpp run_sharded, in-process sharding) run
 under the sanitizer too; a 1 MiB QSMD5_SHARD_BYTES makes even these small
 batches split, and QSMD5_MAPS_AFTER=2 sends the classifier to its
 /proc/self/maps cache from the second pageable query.

@@ -1,7 +1,7 @@
 """CPU test of the host-staging plan (qsfs-fuse_amd/csrc/qsmd5_plan.h).
 
 The plan decides how host-resident chunks are cut into groups, columns and
-ring regions before any H2D copy (qsmd5_runtime.cpp run_batch).  The GPU
+ring regions before any H2D copy (qsmd5_rt_staging.cpp run_batch).  The GPU
 column tests check digests end to end; this test checks the plan's
 invariants directly on the CPU over ~1 700 length mixes, ring sizes, slice
 targets and column widths (tests/cpp/test_plan.cpp): every byte of every
