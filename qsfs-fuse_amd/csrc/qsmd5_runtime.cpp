@@ -1,26 +1,23 @@
-// qsfs-fuse_amd/csrc/qsmd5_runtime.cpp -- host runtime behind include/qsmd5.h.
+// qsfs-fuse_amd/csrc/qsmd5_runtime.cpp -- the C-ABI of include/qsmd5.h.
 //
-// Owns the device, streams, descriptor/digest scratch and the host->device
-// staging ring.  Every entry point is extern "C", catches everything, and
-// reports failure as a negative errno (never an empty digest).  Hashing runs on
-// the gfx950 kernels (md5_kernels.hip) or on the library's own CPU MD5
-// (md5_cpu.h), chosen per call by size, with a CPU fallback when the GPU fails
-// ("backend routing" below).
-//
-// Host-resident batches (the qsfs case: parts sit in pooled host buffers,
-// ResourceManager.cpp:53-77) are cut into slices (a quarter of the batch,
-// clamped to [512 MiB, 4 GiB]); each slice is copied H2D into a ring region on
-// the copy stream and hashed by its own launch on one of kComputeStreams
-// streams, so PCIe transfer of slice k+1 overlaps hashing of slice k.  A slice
-// launch takes one chain time (~85 ms for 10 MiB parts) whatever its size and
-// only ~4 hardware queues run kernels concurrently, so slices are kept large
-// enough that the copy, not kernel concurrency, is the bound.  Staged chunks
-// are packed with a 4 KiB + 256 B skew so that equal-size parts never sit at a
-// power-of-two stride (lanes walk their chunks in lockstep; a power-of-two
-// stride sends every lane's request to the same HBM channel).
-//
-// The runtime itself is in the qsmd5_rt_*.cpp units (qsmd5_rt.h); this file
-// holds the extern "C" entry points and the streaming context.
+// Every entry point is extern "C", catches everything, and reports failure as
+// a negative errno (never an empty digest).  Hashing runs on the gfx950
+// kernels (md5_kernels.hip) or on the library's own CPU MD5 (md5_cpu.h),
+// chosen per call by size, with a CPU fallback when the GPU fails (SURVEY.md
+// §8b, §5).  The runtime behind these entry points is in the qsmd5_rt_*.cpp
+// units (their interface: qsmd5_rt.h):
+//   - qsmd5_rt_device.cpp: the bound GPU(s), their streams, scratch and
+//     staging ring; lazy, fork-aware init; which memory a pointer is;
+//   - qsmd5_rt_staging.cpp: one batch on one GPU.  Host-resident batches (the
+//     qsfs case: parts in pooled host buffers, ResourceManager.cpp:53-77) are
+//     cut into slices, copied H2D into ring regions on copy streams and hashed
+//     by launches on compute streams, the order kept by the calling thread;
+//     staged chunks are packed with a 4 KiB + 256 B skew so that equal-size
+//     parts never sit at a power-of-two stride (a power-of-two stride sends
+//     every lane's request to the same HBM channel);
+//   - qsmd5_rt_route.cpp: group commit of concurrent callers, the backend
+//     routing and its cost model, the CPU backend, split batches.
+// This file holds the entry points and the streaming context (MD5 class).
 #include "qsmd5_rt.h"
 
 using namespace qsmd5::rt;
