@@ -36,7 +36,7 @@ using qsmd5::kNoColumns;
 using qsmd5::stage_bytes;
 
 // The GPU chain rate averaged over timed batches (double bits; 0 = none yet),
-// for the routing cost model ("backend routing" below).  Only a batch that ran
+// for the routing cost model (qsmd5_rt_route.cpp).  Only a batch that ran
 // as ONE latency-kernel launch (<= 16 384 chunks, one chain per lane) with a
 // longest chunk of >= 4 MiB measures a chain: its kernel time is that chain's.
 std::atomic<uint64_t> g_gpu_chain_bits{0};

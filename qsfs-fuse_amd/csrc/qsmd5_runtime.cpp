@@ -24,7 +24,7 @@ using namespace qsmd5::rt;
 
 // ----------------------------------------------------------------------------
 // Streaming context (MD5 class).  One stream is one serial chain, which a host
-// core runs ~6x faster than one GPU lane (the routing rule above), so under
+// core runs ~6x faster than one GPU lane (the routing rule, qsmd5_rt_route.cpp), so under
 // QSMD5_BACKEND=auto or cpu the context hashes on the CPU (md5_cpu.h; device
 // pieces are copied to the host first).  Under QSMD5_BACKEND=gpu the state
 // stays on the device between updates; bytes that do not fill a 64-byte block
