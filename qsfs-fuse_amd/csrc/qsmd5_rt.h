@@ -195,7 +195,7 @@ enum MemKind { kHostMem = 0, kDeviceMem = 1 };
 // *hip_known: HIP knows the pointer (device, pinned or registered host memory).
 MemKind classify(const void* p, int* owner = nullptr, bool* hip_known = nullptr);
 
-// Classifies the chunk pointers of one batch.  The query above costs ~30 ns
+// Classifies the chunk pointers of one batch.  classify()'s query costs ~30 ns
 // for HIP memory and 70-260 ns for pageable memory.  It is serialised inside
 // HIP, so host threads make it slower, not faster
 // (profiles/r01_ubench_classify.log).  Two exact range caches avoid it:
@@ -477,7 +477,7 @@ extern thread_local int t_last_backend;  // qsmd5_last_backend()
 
 int requested_backend(int flags, Backend* b);
 size_t cpu_threads();
-// This host's CPU MD5 rates, timed once (see above).
+// This host's CPU MD5 rates, timed once (qsmd5_rt_route.cpp, "backend routing").
 struct CpuRates {
   double chain = kCpuChainGiBs;  // one thread, one scalar chain
   double lane_thread = 0;        // one thread, its AVX-512 lanes together (0: no AVX-512F)
