@@ -244,3 +244,19 @@ def test_dropin_compiles_with_boost_shared_ptr(tmp_path):
     src = os.path.join(ROOT, "tests", "cpp", "compile_boost_shim.cpp")
     subprocess.check_call(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra", "-w",
                            "-I" + BOOST, src])
+
+
+def test_integration_maps_every_entry_point():
+    """INTEGRATION.md §0 names every function the header declares (and what it
+    replaces in the reference); `name`, `_ex` is the table's shorthand."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    table = text[text.index("## 0. Entry-point map"):text.index("## 1. Build and link")]
+    missing = []
+    for name in declared_functions():
+        short = name[:-3] if name.endswith("_ex") else None
+        if "`%s`" % name in table:
+            continue
+        if short and "`%s`, `_ex`" % short in table:
+            continue
+        missing.append(name)
+    assert not missing, missing
