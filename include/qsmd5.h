@@ -153,6 +153,12 @@ QSMD5_API int qsmd5_set_log_callback(qsmd5_log_fn fn, void* user);
  * initialise the runtime. */
 QSMD5_API int qsmd5_device_count(void);
 
+/* HIP's per-thread error state: the library reads and clears the calling
+ * thread's last HIP error (hipGetLastError) before its own launches, so that a
+ * stale failure of an earlier HIP call -- the caller's or its own -- cannot
+ * fail a good batch.  A caller that wants its own last error must read it
+ * before calling into this library. */
+
 /* Static text for an error code returned by this library. */
 QSMD5_API const char* qsmd5_strerror(int err);
 

@@ -930,9 +930,18 @@ extern "C" __global__ __launch_bounds__(256) void qsmd5_gather_kernel(const Gath
 
 namespace qsmd5 {
 
+// Each launcher returns hipGetLastError() after its launch, and that reports
+// the last failure of ANY HIP call on the thread: a stale one -- the runtime's
+// own out-of-memory hipMalloc before a CPU fallback, or the caller's -- would
+// fail a good launch (and every later one until read).  So each launcher
+// clears it first (clear_stale_error), and the launch's own status is what
+// comes back.
+static inline void clear_stale_error() { (void)hipGetLastError(); }
+
 hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, uint32_t* digests,
                         int kind, hipStream_t s, uint32_t skew_blocks, bool load_nt, uint32_t lanes) {
   if (n == 0) return hipSuccess;
+  clear_stale_error();
   const uint32_t groups = (n + 63u) / 64u;
   if (lanes < 1 || lanes > 64) return hipErrorInvalidValue;
   const uint32_t pc_groups = (n + lanes - 1) / lanes;
@@ -965,6 +974,7 @@ hipError_t launch_batch(const void* chunks, const uint32_t* order, uint32_t n, u
 hipError_t launch_column(const void* segs, const uint32_t* order, uint32_t n, uint32_t* digests,
                          uint64_t col_off, uint64_t col_w, uint32_t* states, hipStream_t s) {
   if (n == 0) return hipSuccess;
+  clear_stale_error();
   if (n > kLatencyKernelResident)  // beyond one resident round: two workgroups per CU
     hipLaunchKernelGGL(qsmd5_column_pc2_kernel, dim3((n + 63u) / 64u), dim3(128), 0, s,
                        static_cast<const ChunkDesc*>(segs), order, n, digests, col_off, col_w,
@@ -981,6 +991,7 @@ hipError_t launch_gather(const void* rows, uint32_t nrows, hipStream_t s, uint32
   if (nrows == 0) return hipSuccess;
   constexpr size_t kGatherLds = 80u << 10;  // keeps latency-kernel workgroups off these CUs
   if (groups == 0) groups = 1;
+  clear_stale_error();
   hipLaunchKernelGGL(qsmd5_gather_kernel, dim3(nrows < groups ? nrows : groups),
                      dim3(256), kGatherLds, s, static_cast<const GatherRow*>(rows), nrows);
   return hipGetLastError();
@@ -988,6 +999,7 @@ hipError_t launch_gather(const void* rows, uint32_t nrows, hipStream_t s, uint32
 
 hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint64_t total_len,
                         hipStream_t s) {
+  clear_stale_error();
   hipLaunchKernelGGL(qsmd5_final_kernel, dim3(1), dim3(64), 0, s, state, tail, rem, total_len);
   return hipGetLastError();
 }
@@ -996,6 +1008,7 @@ hipError_t launch_final(uint32_t* state, const uint8_t* tail, uint32_t rem, uint
 // instead of on the first hash (first 10 MiB call 107 -> ~85 ms), and fails
 // init early if the device cannot run gfx950 code.
 hipError_t warm_up(hipStream_t s) {
+  clear_stale_error();
   hipLaunchKernelGGL(qsmd5_lcg_fill_kernel, dim3(1), dim3(64), 0, s, nullptr, 0, 0, 0u, 0u, 1);
   return hipGetLastError();
 }
@@ -1007,6 +1020,7 @@ hipError_t launch_lcg_fill(uint8_t* base, uint64_t stride, uint64_t len, uint32_
   const uint64_t threads = segs * nchunks;
   const uint64_t blocks = (threads + 255) / 256;
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  clear_stale_error();
   hipLaunchKernelGGL(qsmd5_lcg_fill_kernel, dim3((uint32_t)blocks), dim3(256), 0, s, base, stride,
                      len, seed0, nchunks, segs);
   return hipGetLastError();

@@ -43,6 +43,7 @@ __attribute__((format(printf, 2, 3))) void log_msg(int level, const char* fmt, .
 }
 
 int hip_fail(hipError_t e, const char* what) {
+  (void)hipGetLastError();  // consumed here: a later launch's status must be its own
   std::string s = std::string(what) + ": " + hipGetErrorString(e);
   return fail(e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? -ENOMEM : -EIO, s);
 }

@@ -37,11 +37,16 @@ def pytest_configure(config):
 # the only ones that run uninstrumented vendor runtimes under TSan/ASan.  They
 # go last, so that under `-x` a failure there can never leave a parity test
 # unrun (round 3: a sanitizer child stopped the suite with 17 tests behind it).
-LAST_FILES = ("test_gpu_sanitizers.py",)
+# The memory-pressure test (another tenant holding nearly all HBM) goes just
+# before them, for the same reason: it depends on the box's free memory.
+LAST_FILES = ("test_gpu_memory_pressure.py", "test_gpu_sanitizers.py")
 
 
 def pytest_collection_modifyitems(session, config, items):
-    items.sort(key=lambda it: os.path.basename(str(it.fspath)) in LAST_FILES)  # stable
+    def rank(it):
+        name = os.path.basename(str(it.fspath))
+        return LAST_FILES.index(name) + 1 if name in LAST_FILES else 0
+    items.sort(key=rank)  # stable
 
 
 def _ensure_built():
