@@ -110,9 +110,16 @@ def test_a_stale_hip_error_on_the_thread_does_not_fail_a_launch():
     import qsmd5
     from oracle_util import lcg_bytes, md5_many
     assert qsmd5.lib().qsmd5_init(0) == 0
-    hip = ctypes.CDLL("/opt/rocm/lib/libamdhip64.so.7")  # the runtime libqsmd5.so links
-    p = ctypes.c_void_p()
-    assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(1 << 60)) != 0  # leaves a stale error
+    # every HIP runtime mapped in THIS process (with torch imported first,
+    # libqsmd5.so's soname resolves to torch's bundled copy): each is left
+    # with a stale error on this thread
+    hip_paths = sorted({ln.split()[-1] for ln in open("/proc/self/maps")
+                        if ln.split() and "libamdhip64.so" in ln.split()[-1]})
+    assert hip_paths, "no HIP runtime mapped"
+    for path in hip_paths:
+        hip = ctypes.CDLL(path)
+        p = ctypes.c_void_p()
+        assert hip.hipMalloc(ctypes.byref(p), ctypes.c_size_t(1 << 60)) != 0
     bufs = [lcg_bytes(1300 + i, (1 << 20) + 7 * i) for i in range(8)]
     chunks = [(ctypes.addressof(b), len(b)) for b in bufs]
     assert qsmd5.hash_batch(chunks, flags=qsmd5.FLAG_GPU_ONLY) == md5_many(chunks)
