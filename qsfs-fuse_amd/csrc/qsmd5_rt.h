@@ -84,6 +84,32 @@ int hip_fail(hipError_t e, const char* what);  // -ENOMEM or -EIO, with HIP's me
 uint64_t env_u64(const char* name, uint64_t dflt);
 double env_gibs(const char* name);  // a positive rate in GiB/s, else 0
 
+// ---- ThreadSanitizer: the pinned allocator's hand-off --------------------------
+// HIP's pinned allocator is not instrumented (host-sanitizer builds,
+// scripts/build_sanitized.sh, instrument only this library): a block one
+// thread frees and another is handed next carries no happens-before TSan can
+// see, and a GPU-box run reported the second owner's first write as racing
+// the first owner's last read.  Every pinned allocation the library makes or
+// hands out acquires one sync object and every free releases it, as the
+// allocator's own lock does.  No code in other builds.
+#if defined(__has_feature)
+#if __has_feature(thread_sanitizer)
+#include <sanitizer/tsan_interface.h>
+#define QSMD5_TSAN 1
+#endif
+#endif
+extern char g_pinned_sync;
+inline void pinned_handed_out() {
+#ifdef QSMD5_TSAN
+  __tsan_acquire(&g_pinned_sync);
+#endif
+}
+inline void pinned_handed_back() {
+#ifdef QSMD5_TSAN
+  __tsan_release(&g_pinned_sync);
+#endif
+}
+
 // ---- bound GPUs and lifetime (qsmd5_rt_device.cpp) ---------------------------
 struct DevBuf {
   void* p = nullptr;
@@ -112,6 +138,7 @@ struct HostPinned {
   int reserve(size_t bytes) {
     if (bytes <= cap) return 0;
     if (p) {
+      pinned_handed_back();
       (void)hipHostFree(p);
       p = nullptr;
       cap = 0;
@@ -122,6 +149,7 @@ struct HostPinned {
       p = nullptr;
       return hip_fail(e, "hipHostMalloc");
     }
+    pinned_handed_out();
     cap = want;
     return 0;
   }

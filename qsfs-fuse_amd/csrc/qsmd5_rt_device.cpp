@@ -7,6 +7,7 @@ namespace qsmd5 {
 namespace rt {
 
 thread_local std::string t_last_error;
+char g_pinned_sync;
 
 int fail(int code, const std::string& what) {
   t_last_error = what;

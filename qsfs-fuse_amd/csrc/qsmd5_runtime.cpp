@@ -222,6 +222,7 @@ int qsmd5_alloc_pinned(size_t bytes, void** out) {
     *out = nullptr;
     if (int rc = ensure_init()) return rc;
     QS_HIP(hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault));
+    pinned_handed_out();
     return 0;
   });
 }
@@ -230,6 +231,7 @@ int qsmd5_free_pinned(void* ptr) {
   return guarded([&] {
     if (!ptr) return 0;
     if (int rc = ensure_init()) return rc;
+    pinned_handed_back();
     QS_HIP(hipHostFree(ptr));
     return 0;
   });

@@ -42,10 +42,6 @@
 #if __has_feature(address_sanitizer)
 #include <sanitizer/allocator_interface.h>  // __sanitizer_purge_allocator
 #endif
-#if __has_feature(thread_sanitizer)
-#include <sanitizer/tsan_interface.h>  // __tsan_acquire / __tsan_release
-#define QS_TSAN 1
-#endif
 #endif
 
 extern "C" void oracle_md5(const uint8_t* p, uint64_t len, uint8_t out[16]);
@@ -77,28 +73,6 @@ void fail(const char* what, int rc, int t, int r) {
   fprintf(stderr, "ERROR %s thread %d round %d: rc %d (%s) %s\n", what, t, r, rc, qsmd5_strerror(rc),
           qsmd5_last_error());
   g_bad.fetch_add(1);
-}
-
-// HIP's pinned allocator is not instrumented: a buffer one thread frees and
-// another is then handed at the same address carry no happens-before that TSan
-// can see, so the second thread's first write "races" the first thread's last
-// read (a GPU-box run reported exactly that, race_stress.cpp case 3 against
-// the oracle's read).  The hand-off through the allocator is made visible
-// here, as the allocator's own lock would: every free releases one sync
-// object and every allocation acquires it (a reused block need not start at
-// the freed one's address).
-char g_pinned_allocator;  // the sync object's address
-void pinned_acquired(void* p) {
-  (void)p;
-#ifdef QS_TSAN
-  __tsan_acquire(&g_pinned_allocator);
-#endif
-}
-void pinned_released(void* p) {
-  (void)p;
-#ifdef QS_TSAN
-  __tsan_release(&g_pinned_allocator);
-#endif
 }
 
 // xorshift: per-thread, deterministic
@@ -215,11 +189,11 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
           else check(heap.data(), len, d, "hash_one(heap)", t, r);
           break;
         }
-        pinned_acquired(p);
+        // (the library makes the pinned allocator's hand-off between threads
+        // visible to TSan: qsmd5_rt.h pinned_handed_out / pinned_handed_back)
         memcpy(p, buf.data() + 7, len);
         if ((rc = qsmd5_hash_one(p, len, d)) != 0) fail("hash_one(pinned)", rc, t, r);
         else check((const uint8_t*)p, len, d, "hash_one(pinned)", t, r);
-        pinned_released(p);
         if ((rc = qsmd5_free_pinned(p)) != 0) fail("free_pinned", rc, t, r);
         break;
       }
