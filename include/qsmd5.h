@@ -172,7 +172,11 @@ QSMD5_API int qsmd5_hash_one(const void* ptr, uint64_t len, uint8_t digest[16]);
 /* Hash n independent chunks (qsfs upload parts) in one GPU batch.
  * digests[i] receives the MD5 of chunks[i].  Synchronous: returns when every
  * digest is in `digests` (host memory).  Host-resident chunks are copied to
- * the GPU in slices that overlap with hashing. */
+ * the GPU in slices that overlap with hashing.  Device-resident chunks are
+ * read on the library's own streams, which are not ordered after work the
+ * caller enqueued on any stream (the legacy default stream included):
+ * synchronise the stream that wrote them first, or hash them on that stream
+ * with qsmd5_hash_batch_device_async. */
 QSMD5_API int qsmd5_hash_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16]);
 
 /* As qsmd5_hash_batch with QSMD5_FLAG_* flags. */
