@@ -195,6 +195,8 @@ struct PrehashOptions {
   // false, no further part is uploaded, every buffer not handed over goes back
   // to the pool, and the call returns with stats.stopped; the caller marks
   // parts [stats.uploaded, end) failed, as :669-671.  Empty: never stop.
+  // With `pipeline` it is also called from the helper thread preparing the
+  // next wave, so it must be thread-safe (ShouldContinue takes a lock).
   std::function<bool()> should_continue;
 };
 
