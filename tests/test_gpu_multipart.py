@@ -115,3 +115,20 @@ def test_gpu_waves_leave_the_host_cores_free(gold, wait):
         assert hashing_cpu < 0.15 * r["wall_s_runs"][-1], r
     else:
         assert hashing_cpu > 0.5 * r["hash_s"], r  # the spin is real: the test would see a regression
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [[], ["--async=2"], ["--cancel-after=9"]], ids=["sync", "async", "cancel"])
+def test_concurrent_files_gpu_waves(gold, mode):
+    """Four files flushed at once through one pinned 32-buffer slab pool, every
+    wave forced onto the GPU, the next wave of each file prepared on its helper
+    thread while its current one uploads: waves of different files meet in the
+    runtime's group commit and share launches.  No deadlock, every digest
+    golden (cancelled: the first 9 of each file), every buffer back."""
+    r = run(["--aligned", "--size=%d" % (32 * 10 * MiB), "--pool=32", "--pinned", "--slab", "--files=4",
+             "--upload-ms=2", "--deadlock-s=60"] + mode, "gpu")
+    want = 9 if "--cancel-after=9" in mode else 32
+    assert r["deadlock"] is False and r["error"] == "", r
+    assert r["pool_free_after"] == 32 and r["gpu_waves"] >= 4 and r["cpu_waves"] == 0, r
+    for m in r["md5_files"]:
+        assert m[:want] == gold[:want] and not any(m[want:]), m
