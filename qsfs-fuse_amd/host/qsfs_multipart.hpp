@@ -212,9 +212,12 @@ struct Wave {
   double gather_s = 0, hash_s = 0;
 };
 
+// Handles already handed over are null (Pool::data() == nullptr) and are
+// skipped: a real pool must never be given a null buffer back.
 template <class Pool>
 void release_all(Pool& pool, std::vector<typename Pool::buffer_type>& bufs, size_t from = 0) {
-  for (size_t k = from; k < bufs.size(); ++k) pool.release(bufs[k]);
+  for (size_t k = from; k < bufs.size(); ++k)
+    if (Pool::data(bufs[k])) pool.release(bufs[k]);
   bufs.resize(std::min(from, bufs.size()));
 }
 
@@ -356,7 +359,10 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
         ++st.uploaded;
       }
     } catch (...) {
-      detail::release_all(pool, cur.bufs, k + 1);  // parts of this wave never handed over
+      // parts of this wave never handed over: from k on (a throwing upload()'s
+      // own buffer is already back and null; a throwing should_continue() or
+      // hex formatting left bufs[k] still held)
+      detail::release_all(pool, cur.bufs, k);
       drain_ahead();
       throw;
     }

@@ -316,6 +316,7 @@ int main(int argc, char** argv) {
   double upload_ms = 0, deadlock_s = 20;
   uint32_t short_read_part = 0, fail_upload_part = 0;  // fault injection (1-based part numbers)
   size_t cancel_after = SIZE_MAX;  // each file's transfer is cancelled once it handed this many parts on
+  size_t check_throws_after = SIZE_MAX;  // fault injection: should_continue() throws from then on
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&](const char* key) { return a.rfind(key, 0) == 0 ? a.c_str() + strlen(key) : nullptr; };
@@ -333,6 +334,7 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--short-read-part=")) short_read_part = (uint32_t)strtoul(v, nullptr, 0);
     else if (const char* v = val("--fail-upload-part=")) fail_upload_part = (uint32_t)strtoul(v, nullptr, 0);
     else if (const char* v = val("--cancel-after=")) cancel_after = strtoull(v, nullptr, 0);
+    else if (const char* v = val("--check-throws-after=")) check_throws_after = strtoull(v, nullptr, 0);
     else if (a == "--aligned") aligned = true;
     else if (a == "--pinned") pinned = true;
     else if (a == "--slab") slab = true;
@@ -447,6 +449,11 @@ int main(int argc, char** argv) {
           // --cancel-after: TransferHandle::Cancel from another thread once K parts went out
           std::atomic<size_t> handed{0};
           if (cancel_after != SIZE_MAX) opt.should_continue = [&] { return handed.load() < cancel_after; };
+          if (check_throws_after != SIZE_MAX)
+            opt.should_continue = [&] {
+              if (handed.load() >= check_throws_after) throw std::runtime_error("injected should_continue failure");
+              return true;
+            };
           InFlight inflight;
           auto read = [&](const qsmd5_part& p, char* dst) {
             const size_t got = pf.read(p.offset, p.size, dst);
@@ -469,7 +476,12 @@ int main(int argc, char** argv) {
               inflight.done();
             });
           };
-          st[f] = qsmd5::upload_parts_prehashed(parts, shared, read, upload, opt);
+          try {
+            st[f] = qsmd5::upload_parts_prehashed(parts, shared, read, upload, opt);
+          } catch (...) {
+            inflight.wait();  // parts handed over before the failure are still uploading
+            throw;
+          }
           inflight.wait();
           if (st[f].uploaded != handed.load()) errors[f] = "stats.uploaded disagrees with the parts uploaded";
         } catch (const std::exception& e) {
@@ -487,7 +499,7 @@ int main(int argc, char** argv) {
   }
   finished.store(true);
   watchdog.join();
-  const bool injected = short_read_part || fail_upload_part;
+  const bool injected = short_read_part || fail_upload_part || check_throws_after != SIZE_MAX;
   for (size_t f = 0; f < files; ++f)
     if (!errors[f].empty()) {
       fprintf(stderr, "upload of file %zu failed: %s\n", f, errors[f].c_str());

@@ -131,6 +131,8 @@ def test_concurrent_files_under_tsan(mode):
     ("--fail-upload-part=7", [], 6),
     ("--fail-upload-part=7", ["--async=2"], 6),
     ("--short-read-part=20", ["--async=3"], None),
+    ("--check-throws-after=5", [], 5),            # the cancel check itself throws mid-wave
+    ("--check-throws-after=5", ["--async=2"], 5),
 ])
 def test_failures_stop_the_upload_and_return_every_buffer(fault, mode, want_uploaded):
     """A short read (File::ReadNoLoad found a hole) or a failed upload stops
@@ -144,7 +146,9 @@ def test_failures_stop_the_upload_and_return_every_buffer(fault, mode, want_uplo
     out = run_raw(args, "cpu", timeout=120)
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads(out.stdout)
-    bad = int(fault.split("=")[1])
+    bad = int(fault.split("=")[1])  # the first part that must not go out (1-based)
+    if fault.startswith("--check-throws-after="):
+        bad += 1  # N parts went out, the check before part N + 1 threw
     assert r["error"], r
     assert r["pool_free_after"] == 4, r
     done = [i for i, h in enumerate(r["md5"]) if h]
