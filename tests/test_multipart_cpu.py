@@ -100,8 +100,10 @@ def test_pipeline_hides_hashing_behind_upload():
 
 
 @pytest.mark.parametrize("mode", [[], ["--async=3"], ["--no-pipeline"], ["--max-wave=2"],
-                                  ["--cancel-after=5"], ["--cancel-after=5", "--async=3"]],
-                         ids=["sync", "async", "no_pipeline", "max_wave_2", "cancel", "cancel_async"])
+                                  ["--cancel-after=5"], ["--cancel-after=5", "--async=3"],
+                                  ["--check-throws-after=5", "--async=3"]],
+                         ids=["sync", "async", "no_pipeline", "max_wave_2", "cancel", "cancel_async",
+                              "check_throws_async"])
 def test_concurrent_files_under_tsan(mode):
     """The drop-in header's threads -- the pipeline's helper thread preparing
     the next wave, the shared pool, the executor's completion handler
@@ -119,7 +121,7 @@ def test_concurrent_files_under_tsan(mode):
     assert "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-8000:]
     assert out.returncode == 0, out.stderr[-3000:]
     r = json.loads(out.stdout)
-    want = 5 if "--cancel-after=5" in mode else 12
+    want = 5 if ("--cancel-after=5" in mode or "--check-throws-after=5" in mode) else 12
     assert r["deadlock"] is False and r["pool_free_after"] == 5, r
     assert all(m[:want] == gold[:want] and not any(m[want:]) for m in r["md5_files"]), r["md5_files"]
 
