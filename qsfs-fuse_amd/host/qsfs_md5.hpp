@@ -92,6 +92,18 @@ using if_stream_ptr = decltype(std::declval<const P&>()->rdbuf(),
 template <class StreamPtr, detail::if_stream_ptr<StreamPtr> = 0>
 std::string md5(const StreamPtr& stream) {
   stream->seekg(0, std::ios_base::beg);
+  // The read position is back at 0 however this returns (MD5.cpp:346), a
+  // hashing failure's exception included.
+  struct Rewind {
+    const StreamPtr& s;
+    ~Rewind() {
+      try {  // a stream with exceptions() set must not throw out of here
+        s->clear();
+        s->seekg(0, std::ios_base::beg);
+      } catch (...) {
+      }
+    }
+  } rewind{stream};
   std::streambuf* sb = stream->rdbuf();
   std::string out;
   if (sb) {
@@ -114,8 +126,6 @@ std::string md5(const StreamPtr& stream) {
   } else {
     out = md5_bytes(nullptr, 0);
   }
-  stream->clear();
-  stream->seekg(0, std::ios_base::beg);
   return out;
 }
 
