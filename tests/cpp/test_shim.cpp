@@ -6,6 +6,7 @@
 // md5(shared_ptr<iostream>) (MD5.cpp:343, 346: read position reset to 0) and
 // the StreamBuf view contract (StreamBuf.cpp:32-48; StreamTest.cpp:131-150:
 // a stream over a 3-byte buffer with lengthToRead=2 exposes "01").
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <memory>
@@ -208,6 +209,26 @@ int main() {
       threw = true;
     }
     expect(threw, "content_md5_from_hex rejects non-hex text");
+  }
+  // 7. md5(stream) that fails (a malformed QSMD5_BACKEND makes every hashing
+  //    call return -EINVAL) throws and still leaves the read position at 0.
+  {
+    const char* prev = getenv("QSMD5_BACKEND");
+    const std::string saved = prev ? prev : "";
+    setenv("QSMD5_BACKEND", "bogus", 1);
+    auto buf = std::make_shared<std::vector<char>>(lcg(99, 4096));
+    std::shared_ptr<std::iostream> s = std::make_shared<ViewStream>(buf, 4000);
+    s->seekg(123, std::ios_base::beg);
+    bool threw = false;
+    try {
+      md5(s);
+    } catch (const qsmd5::Error& e) {
+      threw = e.code() == -EINVAL;
+    }
+    if (prev) setenv("QSMD5_BACKEND", saved.c_str(), 1);
+    else unsetenv("QSMD5_BACKEND");
+    expect(threw, "md5(stream) throws qsmd5::Error(-EINVAL) on a hashing failure");
+    expect(s->tellg() == std::streampos(0), "read position reset to 0 after a failed md5(stream)");
   }
   std::printf("failures %d\n", failures);
   return failures ? 1 : 0;
