@@ -510,3 +510,39 @@ def test_large_batches_select_throughput_kernels(n):
     odd = [(o | 1, L) for o, L in spans]
     want_odd = md5_many([(base + o, L) for o, L in odd])
     assert qsmd5.hash_batch([(dev.data_ptr() + o, L) for o, L in odd]) == want_odd
+
+
+def test_one_long_chain_past_the_two_second_poll():
+    """One 1 GiB chunk is one serial chain of ~8.5 s on a GPU lane: the
+    synchronous call sleeps through most of its estimate and then polls, every
+    1 ms once the batch runs 2 s past its start (wait_stream).  Device- and
+    host-resident (pinned), digest == oracle, and the caller's thread is not
+    spinning meanwhile (its CPU time stays a small part of the wall time)."""
+    import resource
+    import time
+    L = 1 << 30
+    data = lcg_bytes(4711, L)
+    want = md5_ref(data, L)
+    dev = torch.frombuffer(data, dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    for src in ("device", "pinned"):
+        if src == "device":
+            chunk = dev
+        else:
+            p = qsmd5.alloc_pinned(L)
+            ctypes.memmove(p, ctypes.addressof(data), L)
+            chunk = (p, L)
+        c0 = resource.getrusage(resource.RUSAGE_THREAD)
+        t0 = time.time()
+        got = qsmd5.hash_batch([chunk], flags=qsmd5.FLAG_GPU_ONLY)
+        wall = time.time() - t0
+        c1 = resource.getrusage(resource.RUSAGE_THREAD)
+        cpu = (c1.ru_utime - c0.ru_utime) + (c1.ru_stime - c0.ru_stime)
+        if src == "pinned":
+            qsmd5.free_pinned(p)
+        print("%s: 1 GiB chain %.2f s wall, %.3f s of the caller's CPU" % (src, wall, cpu))
+        assert got == [want], src
+        # device: one launch, the caller sleeps and polls; pinned: 4096 column
+        # launches ordered by the host, which wakes per column (a spinning
+        # caller would show cpu ~ wall)
+        assert wall > 2.0 and cpu < (0.2 if src == "device" else 0.5) * wall, (src, wall, cpu)
