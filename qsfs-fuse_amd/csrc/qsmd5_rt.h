@@ -307,6 +307,20 @@ class Classifier {
   // reads by DMA; a pageable first row needs the span inside one host VMA, which
   // HIP reads with the CPU.  The VMA cache of operator() is not used here: a
   // registered subrange of a pageable VMA is HIP memory with a smaller range.
+  // Does [lo, lo + len) run past the end of the HIP allocation that holds lo,
+  // as far as the cache knows it (operator() just remembered the range of a
+  // HIP-known pointer)?  A device chunk that does would send the kernel past
+  // the allocation -- a GPU memory fault, not just a wrong digest -- so the
+  // batch is refused instead.  An allocation whose extent HIP does not report
+  // (no cached range) is let through, as before.
+  bool overruns_allocation(uintptr_t lo, uint64_t len) const {
+    for (int k = 0; k < used_; ++k) {
+      const Range& r = ranges_[(next_ + kRanges - 1 - k) % kRanges];
+      if (r.hip && lo - r.lo < r.size) return len > r.size - (lo - r.lo);
+    }
+    return false;
+  }
+
   bool span_in_one(uintptr_t lo, uintptr_t hi) {
     if (hi <= lo) return true;
     for (int k = 0; k < used_; ++k) {

@@ -547,6 +547,10 @@ int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int f
       if (!len[i] || cls(chunks[i].ptr, &owner) != kDeviceMem) continue;
       if (g_gpu_lost.load())
         return fail(-EIO, "qsmd5: the GPU context is lost; a device-resident chunk cannot be read");
+      // its read-back copy would run past the allocation on the GPU too
+      if (cls.overruns_allocation(reinterpret_cast<uintptr_t>(chunks[i].ptr), len[i]))
+        return fail(-EINVAL, "qsmd5: device chunk " + std::to_string(i) + " (" + std::to_string(len[i]) +
+                                 " bytes) runs past the end of its allocation");
       on_dev[i] = 1;
     }
   }

@@ -128,6 +128,9 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     if (L && kind[i] == kDeviceMem && owner != r.device)
       return fail(-EINVAL, "qsmd5: chunk lives on GPU " + std::to_string(owner) +
                                ", not on a bound GPU (QSMD5_DEVICE/QSMD5_DEVICES)");
+    if (L && kind[i] == kDeviceMem && cls.overruns_allocation(reinterpret_cast<uintptr_t>(chunks[i].ptr), L))
+      return fail(-EINVAL, "qsmd5: device chunk " + std::to_string(i) + " (" + std::to_string(L) +
+                               " bytes) runs past the end of its allocation");
   }
 
   const auto t_classified = std::chrono::steady_clock::now();

@@ -574,12 +574,23 @@ static int ctx_blocks(qsmd5_ctx* c, const uint8_t* p, uint64_t nblk, bool on_dev
   return 0;
 }
 
+// A device piece longer than what is left of its HIP allocation: reading it
+// (kernel or read-back copy) would fault the GPU (Classifier::overruns_allocation).
+static bool device_piece_overruns(const void* ptr, uint64_t len, int owner) {
+  uintptr_t lo = 0;
+  size_t size = 0;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+  return Classifier::hip_range(a, owner, &lo, &size) && len > size - (a - lo);
+}
+
 // CPU context: host pieces directly; device pieces through a bounded host copy.
 static int ctx_update_cpu(qsmd5_ctx* c, const void* ptr, uint64_t len) {
   int owner = -1;
   if (qsmd5_device_count() > 0 && classify(ptr, &owner) == kDeviceMem) {
     if (g_gpu_lost.load())
       return fail(-EIO, "qsmd5: the GPU context is lost; a device-resident piece cannot be read");
+    if (device_piece_overruns(ptr, len, owner))
+      return fail(-EINVAL, "qsmd5: device piece runs past the end of its allocation");
     constexpr uint64_t kPiece = 8ull << 20;
     std::vector<uint8_t> buf((size_t)std::min(len, kPiece));
     for (uint64_t off = 0; off < len; off += kPiece) {
@@ -601,9 +612,10 @@ int qsmd5_ctx_update(qsmd5_ctx* c, const void* ptr, uint64_t len) {
     if (len == 0) return 0;
     if (!ptr) return fail(-EINVAL, "qsmd5: NULL ptr with non-zero len");
     if (c->on_cpu) {
-      // a device piece copied only in part would leave a hole: fail the context
+      // a device piece copied only in part would leave a hole: fail the
+      // context (a piece refused up front, -EINVAL, changed nothing)
       const int rc = ctx_update_cpu(c, ptr, len);
-      if (rc) c->failed = true;
+      if (rc && rc != -EINVAL) c->failed = true;
       return rc;
     }
     if (int rc = ensure_init()) return rc;
@@ -613,6 +625,8 @@ int qsmd5_ctx_update(qsmd5_ctx* c, const void* ptr, uint64_t len) {
     if (dev && owner != primary().device)
       return fail(-EINVAL, "qsmd5: update data lives on GPU " + std::to_string(owner) +
                                ", not on the primary bound GPU");
+    if (dev && device_piece_overruns(ptr, len, owner))
+      return fail(-EINVAL, "qsmd5: device piece runs past the end of its allocation");
     const uint8_t* p = static_cast<const uint8_t*>(ptr);
     uint64_t left = len;
     // From here a failure leaves d_state, tail and total out of step: mark the

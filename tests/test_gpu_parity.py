@@ -546,3 +546,37 @@ def test_one_long_chain_past_the_two_second_poll():
         # launches ordered by the host, which wakes per column (a spinning
         # caller would show cpu ~ wall)
         assert wall > 2.0 and cpu < (0.2 if src == "device" else 0.5) * wall, (src, wall, cpu)
+
+
+def test_device_chunk_past_its_allocation_is_refused(monkeypatch):
+    """A device chunk whose length runs past the end of its HIP allocation
+    would send the kernel -- or the CPU backend's read-back copy -- out of
+    bounds (a GPU memory fault, not a wrong digest): the batch is refused with
+    -EINVAL before any launch or copy, forced onto the GPU, forced onto the
+    CPU, and under auto routing (which sends one small chunk to the CPU).  The
+    same allocation hashed to its last byte is fine.  (A 64 MiB tensor has a
+    torch segment of its own.)"""
+    MiB = 1 << 20
+    t = torch.zeros(64 * MiB, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    base = t.data_ptr()
+    tail = 8192
+    ok = qsmd5.hash_batch([(base + 64 * MiB - tail, tail)], flags=qsmd5.FLAG_GPU_ONLY)
+    assert ok == [md5_ref(bytes(tail))]
+    monkeypatch.setenv("QSMD5_BACKEND", "auto")
+    for flags in (qsmd5.FLAG_GPU_ONLY, qsmd5.FLAG_CPU_ONLY, 0):
+        with pytest.raises(qsmd5.Md5Error) as e:
+            qsmd5.hash_batch([(base + 64 * MiB - tail, tail + 4096)], flags=flags)
+        assert e.value.code == -errno.EINVAL, flags
+        assert "runs past the end of its allocation" in str(e.value), str(e.value)
+    # the MD5 class (a CPU context under auto, a GPU one forced): the piece is
+    # refused, the context is left as it was and hashes on
+    for backend in ("auto", "gpu"):
+        monkeypatch.setenv("QSMD5_BACKEND", backend)
+        m = qsmd5.MD5()
+        m.update(b"abc")
+        with pytest.raises(qsmd5.Md5Error) as e:
+            m.update((base + 64 * MiB - tail, tail + 4096))
+        assert e.value.code == -errno.EINVAL, backend
+        m.update((base + 64 * MiB - tail, tail))
+        assert m.finalize().hexdigest() == md5_ref(b"abc" + bytes(tail)).hex(), backend
