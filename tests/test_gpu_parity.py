@@ -554,29 +554,43 @@ def test_device_chunk_past_its_allocation_is_refused(monkeypatch):
     bounds (a GPU memory fault, not a wrong digest): the batch is refused with
     -EINVAL before any launch or copy, forced onto the GPU, forced onto the
     CPU, and under auto routing (which sends one small chunk to the CPU).  The
-    same allocation hashed to its last byte is fine.  (A 64 MiB tensor has a
-    torch segment of its own.)"""
+    same allocation hashed to its last byte is fine.  The 64 MiB buffer is a
+    hipMalloc of its own, made through the HIP runtime libqsmd5.so uses (a
+    torch tensor may sit inside a larger cached segment, whose end is further
+    out)."""
     MiB = 1 << 20
-    t = torch.zeros(64 * MiB, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-    base = t.data_ptr()
-    tail = 8192
-    ok = qsmd5.hash_batch([(base + 64 * MiB - tail, tail)], flags=qsmd5.FLAG_GPU_ONLY)
-    assert ok == [md5_ref(bytes(tail))]
-    monkeypatch.setenv("QSMD5_BACKEND", "auto")
-    for flags in (qsmd5.FLAG_GPU_ONLY, qsmd5.FLAG_CPU_ONLY, 0):
-        with pytest.raises(qsmd5.Md5Error) as e:
-            qsmd5.hash_batch([(base + 64 * MiB - tail, tail + 4096)], flags=flags)
-        assert e.value.code == -errno.EINVAL, flags
-        assert "runs past the end of its allocation" in str(e.value), str(e.value)
-    # the MD5 class (a CPU context under auto, a GPU one forced): the piece is
-    # refused, the context is left as it was and hashes on
-    for backend in ("auto", "gpu"):
-        monkeypatch.setenv("QSMD5_BACKEND", backend)
-        m = qsmd5.MD5()
-        m.update(b"abc")
-        with pytest.raises(qsmd5.Md5Error) as e:
-            m.update((base + 64 * MiB - tail, tail + 4096))
-        assert e.value.code == -errno.EINVAL, backend
-        m.update((base + 64 * MiB - tail, tail))
-        assert m.finalize().hexdigest() == md5_ref(b"abc" + bytes(tail)).hex(), backend
+    size, tail = 64 * MiB, 8192
+    paths = sorted({ln.split()[-1] for ln in open("/proc/self/maps")
+                    if ln.split() and "libamdhip64.so" in ln.split()[-1]})
+    if len(paths) != 1:
+        pytest.skip("not exactly one HIP runtime mapped: %s" % paths)
+    hip = ctypes.CDLL(paths[0])
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
+    p = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(p), size) == 0
+    try:
+        assert hip.hipMemset(p, 0, size) == 0 and hip.hipDeviceSynchronize() == 0
+        base = p.value
+        ok = qsmd5.hash_batch([(base + size - tail, tail)], flags=qsmd5.FLAG_GPU_ONLY)
+        assert ok == [md5_ref(bytes(tail))]
+        monkeypatch.setenv("QSMD5_BACKEND", "auto")
+        for flags in (qsmd5.FLAG_GPU_ONLY, qsmd5.FLAG_CPU_ONLY, 0):
+            with pytest.raises(qsmd5.Md5Error) as e:
+                qsmd5.hash_batch([(base + size - tail, tail + 4096)], flags=flags)
+            assert e.value.code == -errno.EINVAL, flags
+            assert "runs past the end of its allocation" in str(e.value), str(e.value)
+        # the MD5 class (a CPU context under auto, a GPU one forced): the piece
+        # is refused, the context is left as it was and hashes on
+        for backend in ("auto", "gpu"):
+            monkeypatch.setenv("QSMD5_BACKEND", backend)
+            m = qsmd5.MD5()
+            m.update(b"abc")
+            with pytest.raises(qsmd5.Md5Error) as e:
+                m.update((base + size - tail, tail + 4096))
+            assert e.value.code == -errno.EINVAL, backend
+            m.update((base + size - tail, tail))
+            assert m.finalize().hexdigest() == md5_ref(b"abc" + bytes(tail)).hex(), backend
+    finally:
+        hip.hipFree(p)
