@@ -64,3 +64,30 @@ def test_binding_as_printed(doctest_exe, cancel_after):
     r = json.loads(out.stdout.strip().splitlines()[-1])
     sent = 13 if cancel_after < 0 else min(13, cancel_after)
     assert r == {"parts": 13, "sent": sent, "failed": 13 - sent, "pool_free": 5, "bad": 0}, r
+
+
+def test_log_sink_binding_as_printed(tmp_path):
+    """INTEGRATION.md §2's log sink (qsmd5_set_log_callback into qsfs's
+    DebugInfo / DebugWarning / DebugError) compiles as printed, and a hashing
+    call's backend line reaches DebugInfo (CPU backend, no GPU needed)."""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    sec = text[text.index("**The backend in qsfs's own log**"):text.index("## 3. Batch pre-hash")]
+    block = re.findall(r"```cpp\n(.*?)```", sec, re.S)[0]
+    lines = [ln for ln in block.splitlines() if not ln.startswith("#include")]
+    reg = [ln for ln in lines if ln.startswith("qsmd5_set_log_callback(")]
+    assert len(reg) == 1, block
+    fn = "\n".join(ln for ln in lines if ln not in reg)
+    (tmp_path / "fn.inc").write_text(fn + "\n")
+    (tmp_path / "reg.inc").write_text(reg[0] + "\n")
+    exe = str(tmp_path / "log_doctest")
+    subprocess.check_call([
+        "g++", "-std=c++17", "-O1", "-Wall",
+        '-DLOG_SINK_FUNCTION="%s"' % (tmp_path / "fn.inc"), '-DLOG_SINK_REGISTRATION="%s"' % (tmp_path / "reg.inc"),
+        os.path.join(ROOT, "tests", "cpp", "integration_log_doctest.cpp"),
+        "-I" + os.path.join(ROOT, "include"), "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
+        "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-o", exe])
+    env = dict(os.environ, QSMD5_BACKEND="cpu")
+    out = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert "I qsmd5: backend=cpu reason=forced chunks=1 bytes=3" in out.stdout.splitlines(), out.stdout
+    assert out.stderr == "", out.stderr  # the sink takes every line
