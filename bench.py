@@ -491,7 +491,10 @@ def main():
         "per_chain": {"GiBps": round(B * L / (1 << 30) / (kavg_ms * 1e-3) / B, 4),
                       "cycles_per_64B_block_at_2p4GHz": round(kavg_ms * 1e-3 * 2.4e9 / (L / 64), 1),
                       "note": "MD5 is a serial chain per chunk; at batch=512 the job rate is "
-                              "512 x the per-chain rate (SURVEY.md §0 item 5)"},
+                              "512 x the per-chain rate (SURVEY.md §0 item 5)",
+                      "clock_evidence": "the kernel runs at 2.398-2.400 GHz: GRBM_GUI_ACTIVE / 8 XCDs / "
+                                        "wall over its dispatches (profiles/r04_effective_clock.log), so "
+                                        "the 2.4 GHz cycle count above is the kernel's own"},
         "parity": "ok: %d/%d digests == reference golden" % (ntot, ntot) if parity_ok else "FAIL",
         "process_group": pg,
         "cpu_baseline": None,
