@@ -28,6 +28,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "qsfs-fuse_amd"))
 
+from qsmd5.launch import launched, spawn_ranks  # noqa: E402  (no torch, no HIP)
+
 MiB = 1 << 20
 CHUNK = 10 * MiB
 BATCH = 512
@@ -345,6 +347,11 @@ def main():
                          "parts, libqsmd5's CPU backend) and print its JSON line")
     args = ap.parse_args()
 
+    if args.gpus > 1 and not launched():
+        # A bare `bench.py --gpus N` (the driver's command): form the N ranks here,
+        # one fresh process per GPU, before anything touches a GPU.
+        log("bench.py: no launcher environment; starting %d rank processes" % args.gpus)
+        return spawn_ranks(os.path.abspath(__file__), sys.argv[1:], args.gpus)
     if args.cpu_rehearsal:
         return cpu_rehearsal(args)
 
@@ -364,6 +371,9 @@ def main():
         raise SystemExit("bench.py needs a GPU (it measures the gfx950 kernels)")
     if args.rehearse_gloo:
         local = 0
+    elif local >= torch.cuda.device_count():
+        raise SystemExit("rank %d has no GPU of its own (%d visible); --rehearse-gloo runs every "
+                         "rank on cuda:0" % (rank, torch.cuda.device_count()))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     distributed = world > 1 or args.dist_always
@@ -392,13 +402,18 @@ def main():
     desc[:, 0] = data.data_ptr() + torch.arange(B, dtype=torch.int64) * L
     desc[:, 1] = L
     desc = desc.to(dev)
-    dig = torch.zeros((B, 16), dtype=torch.uint8, device=dev)
+    # Two digest tables, alternated by step: the timed steps write into tables
+    # zeroed after the warm-up, and parity checks the first and the last timed
+    # step's own output, so a timed launch that did no work cannot pass on the
+    # warm-up's digests.
+    digs = [torch.zeros((B, 16), dtype=torch.uint8, device=dev) for _ in range(2)]
     torch.cuda.synchronize()
     kernel = {0: "one-wave (qsmd5_batch_kernel)", 1: "producer/consumer (qsmd5_batch_pc64_kernel)",
               2: "coalesced (qsmd5_batch_coal_kernel)",
               3: "producer/consumer, 64 KiB ring (qsmd5_batch_pc2_kernel)"}[qsmd5.kernel_choice(B)]
 
-    def step(ev=None):
+    def step(k, ev=None):
+        dig = digs[k & 1]
         if ev is not None:
             ev[0].record(stream)
         qsmd5.hash_device(desc.data_ptr(), dig.data_ptr(), B, stream=sp)
@@ -408,8 +423,10 @@ def main():
             return gather_digests(dig, B * world)
         return dig
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
+    for d in digs:  # the timed steps start from zeroed tables
+        d.zero_()
     torch.cuda.synchronize()
     events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(args.steps)]
@@ -417,9 +434,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    out = None
+    first = out = None
     for k in range(args.steps):
-        out = step(events[k])
+        out = step(k, events[k])
+        if k == 0:
+            first = out  # a reference: for N > 1 the gather's own tensor, else digs[0]
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -435,10 +454,11 @@ def main():
 
     # --- parity: every digest of the job against the reference-produced fixture -------
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_10MiB.json")))["md5"]
-    table = out if out is not None else dig
+    table = out
     got_hex = [bytes(r).hex() for r in table.cpu().numpy()]
+    first_hex = [bytes(r).hex() for r in first.cpu().numpy()]
     ntot = B * world
-    parity_ok = ntot <= len(gold) and got_hex[:ntot] == gold[:ntot]
+    parity_ok = ntot <= len(gold) and got_hex[:ntot] == gold[:ntot] and first_hex[:ntot] == gold[:ntot]
     if rank == 0 and not parity_ok:
         bad = [i for i in range(min(ntot, len(gold))) if got_hex[i] != gold[i]]
         log("PARITY FAILURE: %d of %d digests differ (first %s)" % (len(bad), ntot, bad[:5]))
@@ -499,6 +519,10 @@ def main():
         "process_group": pg,
         "cpu_baseline": None,
     }
+    if world > 1:
+        result["launcher"] = ("bench.py: %d child processes, one per GPU" % world
+                              if os.environ.get("QSMD5_SPAWNED_BY") == "bench" else
+                              "external (torch.distributed.run or equivalent)")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         host = data.cpu().numpy()
         chunks = [host[i * L:(i + 1) * L].ctypes.data for i in range(B)]
@@ -507,7 +531,7 @@ def main():
         if not cb["agrees_with_gpu"]:
             result["parity"] = "FAIL (cpu reference disagrees)"
         del host
-    del data, desc, dig, out, table
+    del data, desc, digs, out, first, table
     torch.cuda.empty_cache()
     c5_ok = True
     if not args.no_config5:

@@ -84,7 +84,11 @@ _lib = None
 # qsmd5_log_fn: void (*)(int level, const char* msg, void* user)
 LOG_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p)
 LOG_INFO, LOG_WARN, LOG_ERROR = 0, 1, 2  # qsfs LogLevel::Value (base/LogLevel.h:27)
-_log_keep = None  # the installed ctypes callback must outlive every call that may log
+# Every ctypes callback ever installed, for the life of the process: the
+# library never frees a replaced sink because another thread may have loaded it
+# and be about to call it (qsmd5_rt_device.cpp), so the code it points at must
+# not be freed either.  A few hundred bytes per installed sink.
+_log_keep = []
 
 
 def lib():
@@ -187,13 +191,12 @@ def set_log_callback(fn):
     """qsmd5_set_log_callback: route the library's messages to fn(level, text)
     (level LOG_INFO / LOG_WARN / LOG_ERROR) instead of stderr; None restores
     the default.  fn runs on the thread that made the qsmd5 call."""
-    global _log_keep
     if fn is None:
         _check(lib().qsmd5_set_log_callback(LOG_FN(), None), "qsmd5_set_log_callback")
         return
     cb = LOG_FN(lambda level, msg, _user: fn(level, msg.decode(errors="replace")))
+    _log_keep.append(cb)  # before the library can call it; never dropped (see _log_keep)
     _check(lib().qsmd5_set_log_callback(cb, None), "qsmd5_set_log_callback")
-    _log_keep = cb  # kept (never freed while set; a replaced one may still be running)
 
 
 def kernel_choice(n, flags=0):

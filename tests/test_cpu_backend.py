@@ -326,6 +326,46 @@ def test_log_callback_carries_backend_without_stderr():
         assert any(m.startswith("qsmd5: backend=cpu reason=fallback chunks=40") for _, m in lines), out.stdout
 
 
+SINK_SWAP_SCRIPT = r'''
+import gc, threading
+import qsmd5
+stop = threading.Event()
+errors = []
+def hasher():
+    try:
+        while not stop.is_set():
+            qsmd5.hash_batch([b"abc"] * 4, flags=qsmd5.FLAG_CPU_ONLY)  # logs through the sink
+    except Exception as e:
+        errors.append(e)
+threads = [threading.Thread(target=hasher) for _ in range(3)]
+for t in threads:
+    t.start()
+seen = [0]
+for k in range(400):
+    qsmd5.set_log_callback(lambda level, msg, k=k: seen.__setitem__(0, seen[0] + 1))
+    if k % 50 == 0:
+        qsmd5.set_log_callback(None)
+    gc.collect()  # a replaced thunk freed here would be called by a hashing thread
+stop.set()
+for t in threads:
+    t.join()
+assert not errors, errors
+print("swaps ok, %d messages" % seen[0])
+'''
+
+
+def test_log_sink_swaps_while_threads_hash():
+    """ADVICE r04: a replaced sink may still be running on another thread (the
+    library never frees it), so the binding keeps every ctypes thunk it ever
+    installed; 400 swaps under three hashing threads, with a garbage
+    collection after each, must not crash."""
+    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "qsfs-fuse_amd"))
+    out = subprocess.run(["python", "-c", SINK_SWAP_SCRIPT], env=env, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "swaps ok" in out.stdout
+
+
 def test_product_library_does_not_carry_the_oracle():
     """The CPU backend is the library's own code: libqsmd5.so neither links
     the oracle nor exports or contains its symbols."""

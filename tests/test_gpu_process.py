@@ -47,19 +47,20 @@ sys.exit(0 if child_ok and parent_ok else 1)
 '''
 
 SHUTDOWN_SCRIPT = r'''
-import ctypes, hashlib, os, sys
+import ctypes, os, sys
 import qsmd5
+from oracle_util import md5_ref  # the pinned oracle (tests/test_oracle.py)
 buf = bytearray(os.urandom((3 << 20) + 5))
 view = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
 addr = ctypes.addressof(view)
-want = [hashlib.md5(bytes(buf)).digest(), hashlib.md5(bytes(buf[7:1000007])).digest()]
+want = [md5_ref(bytes(buf)), md5_ref(bytes(buf[7:1000007]))]
 chunks = [(addr, len(buf)), (addr + 7, 1000000)]
 for cycle in range(3):
     qsmd5.register_host(addr, len(buf))          # (re)initialises the runtime
     p = qsmd5.alloc_pinned(1 << 20)
     ctypes.memmove(p, addr, 1 << 20)
     got = qsmd5.hash_batch(chunks + [(p, 1 << 20)])
-    assert got[:2] == want and got[2] == hashlib.md5(bytes(buf[:1 << 20])).digest(), cycle
+    assert got[:2] == want and got[2] == md5_ref(bytes(buf[:1 << 20])), cycle
     qsmd5.free_pinned(p)
     if cycle == 2:
         qsmd5.unregister_host(addr)              # the caller's own unregister, then
@@ -184,7 +185,7 @@ def test_shutdown_releases_and_reinitialises(devices):
     """qsmd5_shutdown (a daemon's exit path): three cycles of register a
     pageable buffer + pinned pool + batch + shutdown; each later call
     re-initialises, a registration released by shutdown can be made again,
-    and every digest matches hashlib.  "0,0" binds two contexts to the GPU."""
+    and every digest matches the oracle.  "0,0" binds two contexts to the GPU."""
     env = dict(ENV)
     env.pop("QSMD5_DEVICES", None)
     if devices:
@@ -310,3 +311,44 @@ def test_bench_rccl_path_world_one():
         assert pg["backend"] == "nccl" and pg["world_size"] == 1 and pg["distinct_gpus"] == 1
         assert pg["ranks"][0]["pci"] is not None
     assert r["process_group"]["ranks"][0]["parts"] == 64 and c5["process_group"]["ranks"][0]["parts"] == 32
+
+
+def _bare_env():
+    """The driver's environment for `python bench.py --gpus N`: no launcher variables."""
+    env = dict(ENV)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def test_bench_forms_two_ranks_itself_on_the_card():
+    """`bench.py --gpus 2 --rehearse-gloo` with no launcher in front (VERDICT r04
+    item 1): bench.py starts both rank processes itself; they share the box's
+    one card over gloo and the group reports two ranks."""
+    cmd = [PY, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "64", "--rehearse-gloo", "--config5-parts", "40", "--config5-reps", "1"]
+    out = subprocess.run(cmd, env=_bare_env(), capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["parity"].startswith("ok: 128/128")
+    assert r["launcher"] == "bench.py: 2 child processes, one per GPU"
+    pg = r["process_group"]
+    assert pg["world_size"] == 2 and [x["rank"] for x in pg["ranks"]] == [0, 1]
+    assert r["config5_host"]["parts_per_rank"] == [20, 20]
+
+
+def test_bench_parity_checks_the_timed_steps_own_digests():
+    """the digest tables are zeroed after the warm-up and
+    the first and last timed steps write to different tables, so parity holds
+    only if the timed launches themselves produced every digest."""
+    cmd = [PY, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1", "--no-config5",
+           "--no-cpu-baseline"]
+    out = subprocess.run(cmd, env=_bare_env(), capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-4000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 1 and r["parity"] == "ok: 512/512 digests == reference golden"
+    assert "launcher" not in r  # the N = 1 line keeps BENCH_r03's keys

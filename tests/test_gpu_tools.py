@@ -2,9 +2,8 @@
 
 Files are sliced like QSTransferManager::PrepareUpload, gathered into pinned
 buffers and hashed in one qsmd5_hash_batch call; every printed digest is
-checked against hashlib on the same byte range.
+checked against the pinned oracle on the same byte range.
 """
-import hashlib
 import os
 import subprocess
 import tempfile
@@ -13,14 +12,14 @@ import pytest
 
 import qsmd5
 from conftest import ROOT
-from oracle_util import lcg_bytes
+from oracle_util import lcg_bytes, md5_ref
 
 pytestmark = pytest.mark.gpu
 MiB = 1 << 20
 TOOL = os.path.join(ROOT, "qsfs-fuse_amd", "bin", "qsmd5sum")
 
 
-def test_qsmd5sum_parts_match_hashlib():
+def test_qsmd5sum_parts_match_oracle():
     if not os.path.exists(TOOL):
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "qsfs-fuse_amd")])
     sizes = [0, 5, 19 * MiB, 20 * MiB, 21 * MiB + 3, 25 * MiB, 64 * MiB + 1]
@@ -40,11 +39,11 @@ def test_qsmd5sum_parts_match_hashlib():
         for p, b in zip(paths, blobs):
             parts = qsmd5.plan_parts(len(b))
             if len(parts) == 1 and len(b) < 20 * MiB:
-                want.append("%s  %s" % (hashlib.md5(b).hexdigest(), p))
+                want.append("%s  %s" % (md5_ref(b).hex(), p))
             else:
                 for q in parts:
                     want.append("%s  %s#%d %d %d" % (
-                        hashlib.md5(b[q.offset:q.offset + q.size]).hexdigest(), p,
+                        md5_ref(b[q.offset:q.offset + q.size]).hex(), p,
                         q.part_number, q.offset, q.size))
         assert lines == want
         # -b 1: 1 MiB parts (the -b option of qsfs, Parser.cpp:167)
