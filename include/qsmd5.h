@@ -276,6 +276,35 @@ QSMD5_API int qsmd5_plan_parts(uint64_t file_size, uint64_t buf_size, uint64_t m
  * at the byte for parts[0].offset (host or device memory). */
 QSMD5_API int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t n, uint8_t (*digests)[16]);
 
+/* Pull-driven batch: hash n chunks that are NOT whole buffers in memory -- a
+ * qsfs file's parts, held in its page cache and gathered by File::ReadNoLoad
+ * (src/data/File.cpp:308-375), the read QSTransferManager::DoMultiPartUpload
+ * makes for every part before it hashes it (QSTransferManager.cpp:621-623,
+ * MD5 at QSClient.cpp:369-371).  The library asks for the bytes through
+ * `read` in COLUMN WINDOWS into its own pinned staging: every chunk of a group
+ * (up to 32 768) is one GPU chain that parks its state between windows, so the
+ * batch is as wide as the file has parts while the staging never exceeds
+ * `staging_bytes` (0: QSMD5_READ_STAGING_BYTES, default 256 MiB), whatever the
+ * file's size.  The reader fills the next window while the GPU copies and
+ * hashes the last one.
+ *
+ *   read(user, chunk, offset, len, dst): copy bytes [offset, offset + len) of
+ *   chunk `chunk` (0-based index into lens) to dst and return the number of
+ *   bytes copied, as ReadNoLoad's readSize.  Any other count than len fails the
+ * *   call with -EIO (the reference stops the upload on a short read,
+ *   QSTransferManager.cpp:625-643); nothing is hashed from it.
+ *
+ * read runs on the calling thread only, one window at a time, with each
+ * chunk's windows in increasing offset order and every byte asked for once --
+ * except that in QSMD5_BACKEND=auto a GPU failure re-runs the whole batch on
+ * the CPU, asking for every byte again from offset 0.  It may call other qsmd5
+ * entry points (not qsmd5_shutdown).  lens[i] < 2^38.  Routed like
+ * qsmd5_hash_batch_ex (flags: QSMD5_FLAG_GPU_ONLY / _CPU_ONLY /
+ * _REF_TRUNCATE32); on the GPU the first bound GPU hashes it. */
+typedef uint64_t (*qsmd5_read_fn)(void* user, size_t chunk, uint64_t offset, uint64_t len, void* dst);
+QSMD5_API int qsmd5_hash_read(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* user,
+                              uint64_t staging_bytes, uint8_t (*digests)[16], int flags);
+
 /* Download-side integrity (new: the reference never
  * hashes downloads).  QSClient::DownloadFile keeps the object's ETag
  * (QSClient.cpp:321-323) and ReceivedHandlerSingleDownload

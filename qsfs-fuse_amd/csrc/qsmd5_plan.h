@@ -304,4 +304,73 @@ inline int pipeline_turn(size_t S, size_t nregions, bool meta, PipelineState& st
   return moved ? 1 : 0;
 }
 
+// ---- pull-driven batches (qsmd5_hash_read, qsmd5_rt_read.cpp) -----------------
+// The chunks are not in memory as whole buffers (a qsfs file's parts live in
+// its page cache, File::ReadNoLoad gathers them, File.cpp:308-375): the
+// library asks for them in COLUMN WINDOWS and hashes each window as it lands,
+// every chain parking its state between windows.  The staging budget B is
+// split into two host regions (the reader fills one while the other is copied
+// to the GPU) and one device region; a region holds one column of a GROUP of
+// up to `rows_max` chunks, row k at stride stage_bytes(W).  So the GPU's width
+// (one chain per chunk in a group) depends on the budget only through the
+// column width W, never on how many whole chunks fit: 512 x 10 MiB parts go in
+// ONE group of 512 chains through 512 MiB of staging (21 columns of 508 KiB),
+// and a 100 GB object never stages more than B.
+constexpr uint64_t kReadColMin = 64ull << 10;   // narrowest column: ~1 K blocks per launch
+constexpr uint64_t kReadColsTarget = 8;         // columns per group when the budget allows
+constexpr size_t kReadMaxRows = 32768;          // one resident round of the column kernels
+
+struct ReadGroup {
+  size_t first, count;  // lanes [first, first + count) of the longest-first order
+  uint64_t W;           // column width (a multiple of 64)
+  uint64_t stride;      // row pitch in a region: stage_bytes(W)
+  uint32_t ncols;
+};
+
+struct ReadPlan {
+  uint64_t region = 0;  // bytes of one staging region
+  std::vector<ReadGroup> groups;
+  // Lanes of group g live in column j: a prefix (lengths are longest first);
+  // column 0 holds every lane, empty chunks included (they finish there).
+  static size_t active(const std::vector<uint64_t>& len, const ReadGroup& g, uint32_t j) {
+    if (j == 0) return g.count;
+    size_t a = 0;
+    while (a < g.count && len[g.first + a] > (uint64_t)j * g.W) ++a;
+    return a;
+  }
+  // Bytes of lane k's chunk (length L) in column j of its group.
+  static uint64_t col_bytes(const ReadGroup& g, uint64_t L, uint32_t j) {
+    const uint64_t o = (uint64_t)j * g.W;
+    return L > o ? std::min(g.W, L - o) : 0;
+  }
+};
+
+// len: chunk lengths in lane order, longest first.  staging: the budget B.
+inline ReadPlan plan_read(const std::vector<uint64_t>& len, uint64_t staging) {
+  ReadPlan P;
+  if (len.empty()) return P;
+  const uint64_t min_row = stage_bytes(kReadColMin);
+  P.region = std::max<uint64_t>(staging / 2, min_row);
+  const size_t rows_max =
+      (size_t)std::max<uint64_t>(1, std::min<uint64_t>(kReadMaxRows, P.region / min_row));
+  for (size_t k = 0; k < len.size();) {
+    ReadGroup g{k, std::min(rows_max, len.size() - k), 0, 0, 1};
+    const uint64_t L0 = len[k];
+    // the widest W whose rows all fit one region: count x (W + kSkew) <= region
+    const uint64_t per = P.region / g.count;  // >= min_row
+    const uint64_t w_budget = (per - kSkew) / kAlign * kAlign;
+    const uint64_t per_col = (L0 + kReadColsTarget - 1) / kReadColsTarget;
+    const uint64_t w_target = std::max(kReadColMin, (per_col + kColGrain - 1) / kColGrain * kColGrain);
+    uint64_t W = std::min(w_budget, w_target);
+    const uint64_t whole = std::max<uint64_t>(kAlign, (L0 + kAlign - 1) / kAlign * kAlign);
+    if (whole < W) W = whole;  // short chunks: one column
+    g.W = W;
+    g.stride = stage_bytes(W);
+    g.ncols = (uint32_t)std::max<uint64_t>(1, (L0 + W - 1) / W);
+    P.groups.push_back(g);
+    k += g.count;
+  }
+  return P;
+}
+
 }  // namespace qsmd5

@@ -11,6 +11,8 @@
 //   qsmd5_rt_route.cpp    group commit of concurrent callers, backend routing
 //                         and its cost model, the CPU backend, split batches,
 //                         the fallback after a GPU failure
+//   qsmd5_rt_read.cpp     pull-driven batches (qsmd5_hash_read): the caller's
+//                         reads in column windows through pinned staging
 //   qsmd5_runtime.cpp     the extern "C" entry points and the streaming context
 //
 // Everything here lives in qsmd5::rt and is hidden from the shared library's
@@ -190,6 +192,15 @@ struct Dev {
   uint64_t staging_cap = kDefaultStaging;
   double last_wall_ms = 0, last_kernel_ms = 0;
   std::atomic<uint32_t> chain_samples{0};  // batches that qualified as a chain-rate sample
+  // Pull-driven batches (qsmd5_hash_read, qsmd5_rt_read.cpp) have their own
+  // lock, stream and buffers: a job runs for as long as the caller's reads
+  // take, and must not hold `mu` (every other batch on this GPU) meanwhile.
+  std::mutex read_mu;
+  hipStream_t read_stream = nullptr;
+  hipEvent_t read_copied[2] = {};  // the last H2D copy out of host region k
+  hipEvent_t read_done = nullptr;
+  HostPinned h_read, h_read_meta;  // two staging regions; descriptors + orders, then digests
+  DevBuf d_read, d_read_meta, d_read_state, d_read_dig;
 };
 
 struct Runtime {
@@ -441,6 +452,11 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
 int run_sharded(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags,
                 double* kernel_ms, double* wall_ms);
 
+// ---- pull-driven batches (qsmd5_rt_read.cpp) -------------------------------------
+constexpr uint64_t kDefaultReadStaging = 256ull << 20;  // QSMD5_READ_STAGING_BYTES
+int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* user,
+                     uint64_t staging_bytes, uint8_t (*digests)[16], int flags);
+
 // ---- entry-point scope (every extern "C" call that may reach the runtime) -----
 // Entry points leave the calling thread's current HIP device as they found
 // it: the runtime makes its own GPU current, and a torch or HIP thread working
@@ -540,6 +556,8 @@ std::vector<uint32_t> plan_split(const qsmd5_chunk* chunks, size_t n, int flags)
 int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags,
               bool allow_mb = true);
 int hash_routed(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags);
+// After a failed GPU batch: marks the context lost on a sticky HIP error.
+void note_gpu_failure(int rc, bool injected_sticky);
 
 }  // namespace rt
 }  // namespace qsmd5

@@ -132,6 +132,11 @@ static int init_dev(Dev& d, int device) {
       (e = hipEventCreateWithFlags(&d.ev_done, hipEventBlockingSync | hipEventDisableTiming)) !=
           hipSuccess)
     return hip_fail(e, "hipEventCreate");
+  if ((e = hipStreamCreateWithFlags(&d.read_stream, hipStreamNonBlocking)) != hipSuccess)
+    return hip_fail(e, "hipStreamCreate");
+  for (hipEvent_t* ev : {&d.read_copied[0], &d.read_copied[1], &d.read_done})
+    if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
+      return hip_fail(e, "hipEventCreate");
   if ((e = qsmd5::warm_up(d.compute[0])) != hipSuccess ||
       (e = hipStreamSynchronize(d.compute[0])) != hipSuccess)
     return hip_fail(e, "qsmd5: kernel warm-up (is this a gfx950 GPU?)");
@@ -163,18 +168,25 @@ int release_dev(Dev& d) {
       chk(hipStreamDestroy(s));
       s = nullptr;
     }
-  for (hipEvent_t* e : {&d.ev_meta, &d.ev_first, &d.ev_last, &d.ev_done})
+  if (d.read_stream) {
+    chk(hipStreamSynchronize(d.read_stream));
+    chk(hipStreamDestroy(d.read_stream));
+    d.read_stream = nullptr;
+  }
+  for (hipEvent_t* e : {&d.ev_meta, &d.ev_first, &d.ev_last, &d.ev_done, &d.read_copied[0],
+                        &d.read_copied[1], &d.read_done})
     if (*e) {
       chk(hipEventDestroy(*e));
       *e = nullptr;
     }
-  for (DevBuf* b : {&d.d_meta, &d.d_dig, &d.d_staging, &d.d_state})
+  for (DevBuf* b : {&d.d_meta, &d.d_dig, &d.d_staging, &d.d_state, &d.d_read, &d.d_read_meta,
+                    &d.d_read_state, &d.d_read_dig})
     if (b->p) {
       chk(hipFree(b->p));
       b->p = nullptr;
       b->cap = 0;
     }
-  for (HostPinned* b : {&d.h_meta, &d.h_dig})
+  for (HostPinned* b : {&d.h_meta, &d.h_dig, &d.h_read, &d.h_read_meta})
     if (b->p) {
       chk(hipHostFree(b->p));
       b->p = nullptr;

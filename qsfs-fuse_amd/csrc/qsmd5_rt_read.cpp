@@ -1,0 +1,268 @@
+// qsfs-fuse_amd/csrc/qsmd5_rt_read.cpp -- pull-driven batches (qsmd5_hash_read): a
+// file's parts read by the caller in column windows into the library's pinned
+// staging and hashed as the windows land (the runtime's units: qsmd5_rt.h).
+//
+// Why: inside qsfs, DoMultiPartUpload reads each part into
+// a pooled transfer buffer (QSTransferManager.cpp:611-623) and the pool holds
+// -n buffers (TransferManager.h:74-86), so a batch over pool buffers is at most
+// -n parts wide -- 5 at qsfs's default, far below the width at which a GPU
+// batch pays (it costs one chain time, ~85 ms per 10 MiB part, whatever its
+// width).  Here the library owns the staging and asks for the bytes window by
+// window (File::ReadNoLoad, File.cpp:308-375, gathers any byte range of a
+// loaded file), and every part of the file is its own chain, parked between
+// windows: the batch is as wide as the file, the staging stays bounded.
+//
+// Schedule on the GPU (one stream, qsmd5_plan.h plan_read): step s = (group,
+// column).  The calling thread fills host region s % 2 through the caller's
+// reads, then enqueues its H2D copy into the one device region and the column
+// kernel that hashes it.  Stream order keeps the device region safe (copy s+1
+// runs after kernel s); the host waits only before refilling a host region, for
+// the copy that last read it (two steps back), so the reads of step s+1 run
+// while step s copies and hashes.  The reads are the bound: a column kernel of
+// 512 chains x 508 KiB runs in ~4 ms, the copy in ~5 ms, while one thread
+// gathers the 254 MiB in ~20 ms (the page cache's memcpy).
+#include "qsmd5_rt.h"
+
+namespace qsmd5 {
+namespace rt {
+
+namespace {
+
+struct ReadJob {
+  qsmd5_read_fn read;
+  void* user;
+  std::vector<uint64_t> len;     // hashed length of each chunk (REF_TRUNCATE32 applied)
+  std::vector<uint32_t> order;   // lane -> chunk, longest first (ties by index)
+  std::vector<uint64_t> sorted;  // len[order[k]]
+  uint64_t total = 0;
+  bool short_read = false;       // the caller's read came back short: not a GPU failure
+};
+
+// The window of column j of group g for its `active` live lanes, lane k at
+// dst + k * stride.  A count other than asked fails the job (-EIO), as a short
+// ReadNoLoad stops the reference's upload (QSTransferManager.cpp:625-643).
+int fill_window(ReadJob& J, const ReadGroup& g, uint32_t j, size_t active, uint8_t* dst) {
+  const uint64_t off = (uint64_t)j * g.W;
+  for (size_t k = 0; k < active; ++k) {
+    const uint32_t c = J.order[g.first + k];
+    const uint64_t w = ReadPlan::col_bytes(g, J.len[c], j);
+    if (!w) continue;
+    const uint64_t got = J.read(J.user, c, off, w, dst + k * g.stride);
+    if (got != w) {
+      J.short_read = true;
+      return fail(-EIO, "qsmd5_hash_read: short read of chunk " + std::to_string(c) + " at offset " +
+                            std::to_string(off) + ": " + std::to_string(got) + " of " +
+                            std::to_string(w) + " bytes");
+    }
+  }
+  return 0;
+}
+
+// Wait for `ev` without holding a core: poll, sleeping 20 us backing off to 500 us.
+int poll_event(hipEvent_t ev, const char* what) {
+  int idle_us = 20;
+  for (;;) {
+    const hipError_t q = hipEventQuery(ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) return hip_fail(q, what);
+    std::this_thread::sleep_for(std::chrono::microseconds(idle_us));
+    idle_us = std::min(500, idle_us * 2);
+  }
+}
+
+int gpu_read(Dev& r, ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
+  std::lock_guard<std::mutex> lk(r.read_mu);
+  const size_t n = J.len.size();
+  const ReadPlan P = plan_read(J.sorted, staging);
+  uint64_t region = 0;
+  for (const ReadGroup& g : P.groups) region = std::max<uint64_t>(region, g.count * g.stride);
+  const size_t desc_span = (n * sizeof(qsmd5_chunk) + 255) & ~size_t(255);
+  const size_t meta_bytes = desc_span + n * sizeof(uint32_t);
+  if (int rc = r.h_read.reserve(2 * region)) return rc;
+  if (int rc = r.d_read.reserve(region)) return rc;
+  if (int rc = r.h_read_meta.reserve(std::max<size_t>(meta_bytes, 16 * n))) return rc;
+  if (int rc = r.d_read_meta.reserve(meta_bytes)) return rc;
+  if (int rc = r.d_read_state.reserve(16 * n)) return rc;
+  if (int rc = r.d_read_dig.reserve(16 * n)) return rc;
+  uint8_t* hm = static_cast<uint8_t*>(r.h_read_meta.p);
+  uint8_t* dm = static_cast<uint8_t*>(r.d_read_meta.p);
+  uint8_t* dstage = static_cast<uint8_t*>(r.d_read.p);
+  // Lane k of group g reads its window from the device region's row k; the
+  // descriptor carries the chunk's whole length (the column kernel's segment
+  // form: it finishes the chain in the column that holds the chunk's end).
+  qsmd5_chunk* hd = reinterpret_cast<qsmd5_chunk*>(hm);
+  uint32_t* ho = reinterpret_cast<uint32_t*>(hm + desc_span);
+  for (const ReadGroup& g : P.groups)
+    for (size_t k = 0; k < g.count; ++k) {
+      const uint32_t c = J.order[g.first + k];
+      hd[g.first + k] = qsmd5_chunk{dstage + k * g.stride, J.len[c]};
+      ho[g.first + k] = c;
+    }
+  const hipStream_t s = r.read_stream;
+  // After a failure, let everything enqueued finish before returning: a copy
+  // may still be reading a host region the next call refills.
+  auto drain = [&](int rc) {
+    (void)hipStreamSynchronize(s);
+    return rc;
+  };
+  auto hip = [&](hipError_t e, const char* what) { return e == hipSuccess ? 0 : hip_fail(e, what); };
+  if (int rc = hip(hipMemcpyAsync(dm, hm, meta_bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync H2D"))
+    return drain(rc);
+  const qsmd5_chunk* d_desc = reinterpret_cast<const qsmd5_chunk*>(dm);
+  const uint32_t* d_ord = reinterpret_cast<const uint32_t*>(dm + desc_span);
+  uint32_t* d_dig = static_cast<uint32_t*>(r.d_read_dig.p);
+  uint32_t* d_state = static_cast<uint32_t*>(r.d_read_state.p);
+  uint8_t* hstage = static_cast<uint8_t*>(r.h_read.p);
+  size_t step = 0;
+  for (const ReadGroup& g : P.groups)
+    for (uint32_t j = 0; j < g.ncols; ++j, ++step) {
+      const int reg = (int)(step & 1);
+      uint8_t* host = hstage + reg * region;
+      if (step >= 2)  // the copy that last read this region (step - 2) has finished
+        if (int rc = poll_event(r.read_copied[reg], "qsmd5_hash_read: staging copy")) return drain(rc);
+      const size_t act = ReadPlan::active(J.sorted, g, j);
+      if (int rc = fill_window(J, g, j, act, host)) return drain(rc);
+      if (int rc = hip(hipMemcpyAsync(dstage, host, act * g.stride, hipMemcpyHostToDevice, s),
+                       "hipMemcpyAsync H2D"))
+        return drain(rc);
+      if (int rc = hip(hipEventRecord(r.read_copied[reg], s), "hipEventRecord")) return drain(rc);
+      if (int rc = hip(qsmd5::launch_column(d_desc + g.first, d_ord + g.first, (uint32_t)act, d_dig,
+                                            (uint64_t)j * g.W, g.W, d_state, s),
+                       "qsmd5 column kernel launch"))
+        return drain(rc);
+    }
+  // the metadata's H2D ran first on this stream: its host block is free for the digests
+  if (int rc = hip(hipMemcpyAsync(hm, d_dig, 16 * n, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H"))
+    return drain(rc);
+  if (int rc = hip(hipEventRecord(r.read_done, s), "hipEventRecord")) return drain(rc);
+  if (int rc = poll_event(r.read_done, "qsmd5_hash_read: waiting for the batch")) return drain(rc);
+  memcpy(digests, hm, 16 * n);
+  return 0;
+}
+
+// The CPU backend of a pull-driven batch: the same windows into a host buffer,
+// each window's rows folded into their chunks' running contexts (md5_cpu.h
+// Ctx) on up to cpu_threads() threads.
+int cpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
+  const size_t n = J.len.size();
+  const ReadPlan P = plan_read(J.sorted, staging);
+  uint64_t region = 0;
+  for (const ReadGroup& g : P.groups) region = std::max<uint64_t>(region, g.count * g.stride);
+  std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[std::max<uint64_t>(region, 1)]);
+  if (!buf) return fail(-ENOMEM, "qsmd5_hash_read: host staging allocation failed");
+  std::vector<qsmd5::cpu::Ctx> ctx(n);
+  for (const ReadGroup& g : P.groups)
+    for (uint32_t j = 0; j < g.ncols; ++j) {
+      const size_t act = ReadPlan::active(J.sorted, g, j);
+      if (int rc = fill_window(J, g, j, act, buf.get())) return rc;
+      std::atomic<size_t> next{0};
+      auto work = [&]() noexcept {
+        for (size_t k; (k = next.fetch_add(1)) < act;) {
+          const uint32_t c = J.order[g.first + k];
+          const uint64_t w = ReadPlan::col_bytes(g, J.len[c], j);
+          if (w) ctx[c].update(buf.get() + k * g.stride, w);
+        }
+      };
+      const size_t T = std::min<size_t>({cpu_threads(), act, (size_t)std::max<uint64_t>(1, act * g.W >> 20)});
+      std::vector<std::thread> th;
+      for (size_t t = 1; t < T; ++t) {
+        try {
+          th.emplace_back(work);
+        } catch (...) {
+          break;  // fewer helpers: this thread takes the rest
+        }
+      }
+      work();
+      for (auto& t : th) t.join();
+    }
+  for (size_t c = 0; c < n; ++c) ctx[c].final(digests[c]);
+  return 0;
+}
+
+void log_read(const char* backend, const char* reason, const ReadJob& J) {
+  if (!log_wanted(QSMD5_LOG_INFO)) return;
+  log_msg(QSMD5_LOG_INFO, "qsmd5: backend=%s reason=%s chunks=%zu bytes=%llu (read)", backend, reason,
+          J.len.size(), (unsigned long long)J.total);
+}
+
+}  // namespace
+
+int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* user,
+                     uint64_t staging_bytes, uint8_t (*digests)[16], int flags) {
+  if (n == 0) return 0;
+  if (!lens || !read || !digests) return fail(-EINVAL, "qsmd5_hash_read: NULL lens/read/digests");
+  if (n > 0xffffffffull) return fail(-EINVAL, "qsmd5: too many chunks");
+  Backend b = kAuto;
+  if (int rc = requested_backend(flags, &b)) return rc;
+  ReadJob J;
+  J.read = read;
+  J.user = user;
+  J.len.resize(n);
+  uint64_t longest = 0;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t L = lens[i];
+    if (flags & QSMD5_FLAG_REF_TRUNCATE32) L &= 0xffffffffull;
+    if (L >= kMaxChunkLen) return fail(-EINVAL, "qsmd5: chunk longer than 2^38 bytes");
+    J.len[i] = L;
+    J.total += L;
+    longest = std::max(longest, L);
+  }
+  J.order.resize(n);
+  std::iota(J.order.begin(), J.order.end(), 0u);
+  std::stable_sort(J.order.begin(), J.order.end(),
+                   [&](uint32_t a, uint32_t c) { return J.len[a] > J.len[c]; });
+  J.sorted.resize(n);
+  for (size_t k = 0; k < n; ++k) J.sorted[k] = J.len[J.order[k]];
+  const uint64_t staging = staging_bytes ? staging_bytes
+                                         : env_u64("QSMD5_READ_STAGING_BYTES", kDefaultReadStaging);
+  auto on_cpu = [&](const char* reason) {
+    log_read("cpu", reason, J);
+    const int rc = cpu_read(J, staging, digests);
+    if (rc == 0) {
+      t_last_backend = QSMD5_BACKEND_CPU;
+      g_cpu_batches.fetch_add(1);
+      g_cpu_chunks.fetch_add(n);
+    }
+    return rc;
+  };
+  if (b == kCpu) return on_cpu("forced");
+  if (b == kAuto) {
+    if (g_gpu_lost.load()) return on_cpu("gpu-lost");
+    // the reads cost the same on either backend: price the hashing alone,
+    // as for a batch of host chunks of these lengths
+    if (cpu_est_ms(longest, J.total) < gpu_est_ms(longest, J.total)) return on_cpu("size");
+  }
+  log_read("gpu", b == kGpu ? "forced" : "size", J);
+  int rc = ensure_init();
+  bool sticky = false;
+  if (rc == 0) {
+    const char* inj = getenv("QSMD5_INJECT_GPU_FAULT");
+    if (inj && *inj && strcmp(inj, "0")) {
+      sticky = !strcmp(inj, "sticky");
+      rc = fail(-EIO, "qsmd5: injected GPU fault (QSMD5_INJECT_GPU_FAULT)");
+    } else {
+      rc = gpu_read(primary(), J, staging, digests);
+    }
+  }
+  if (rc == 0) {
+    t_last_backend = QSMD5_BACKEND_GPU;
+    g_gpu_batches.fetch_add(1);
+    g_gpu_chunks.fetch_add(n);
+    return 0;
+  }
+  // Forced GPU: no fallback.  A short read or -EINVAL is the caller's, not the GPU's.
+  if (b == kGpu || rc == -EINVAL || J.short_read) return rc;
+  note_gpu_failure(rc, sticky);
+  const std::string gpu_err = t_last_error;
+  if (rc != -ENODEV)
+    log_msg(QSMD5_LOG_WARN, "qsmd5: GPU read batch of %zu chunks failed (%s); re-reading and hashing "
+            "it on the CPU", n, gpu_err.c_str());
+  J.short_read = false;
+  const int rc2 = on_cpu("fallback");
+  if (rc2) return fail(rc2, t_last_error + " (after GPU failure: " + gpu_err + ")");
+  g_fallbacks.fetch_add(1);
+  return 0;
+}
+
+}  // namespace rt
+}  // namespace qsmd5

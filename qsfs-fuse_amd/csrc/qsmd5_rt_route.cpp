@@ -670,7 +670,7 @@ static void log_call(const char* backend, const char* reason, size_t n, const qs
 // After a failed GPU batch: is the HIP context gone for good (a sticky error
 // such as an illegal address)?  Then every later call goes to the CPU; the
 // daemon keeps producing Content-MD5s until it is restarted.
-static void note_gpu_failure(int rc, bool injected_sticky) {
+void note_gpu_failure(int rc, bool injected_sticky) {
   if (g_gpu_lost.load()) return;
   bool lost = injected_sticky;
   std::string why = injected_sticky ? "injected sticky fault (QSMD5_INJECT_GPU_FAULT=sticky)" : "";

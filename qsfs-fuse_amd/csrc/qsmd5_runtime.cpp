@@ -357,6 +357,11 @@ int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t n, uint8_
   });
 }
 
+int qsmd5_hash_read(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* user, uint64_t staging_bytes,
+                    uint8_t (*digests)[16], int flags) {
+  return guarded([&] { return hash_read_routed(lens, n, read, user, staging_bytes, digests, flags); });
+}
+
 int qsmd5_etag_matches(const uint8_t digest[16], const char* etag) {
   if (!digest || !etag) return fail(-EINVAL, "qsmd5: NULL digest/etag");
   size_t n = strlen(etag);

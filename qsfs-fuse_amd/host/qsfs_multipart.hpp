@@ -333,8 +333,10 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
     if (opt.pipeline && next < parts.size()) {
       try {
         ahead = std::async(std::launch::async, prep, next);
-      } catch (const std::system_error&) {
-        // no thread to spare: this wave uploads, then the next is prepared here
+      } catch (...) {
+        // no thread to spare (std::system_error) or no memory for the shared
+        // state (std::bad_alloc): this wave uploads, then the next is prepared
+        // here; the wave's buffers are still cur's, released as it uploads
       }
     }
     const auto t0 = clock::now();
@@ -382,6 +384,196 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
       cur = prep(next);
       st.wait_s += secs(t1, clock::now());
     }
+  }
+  st.wall_s = secs(t_start, clock::now());
+  return st;
+}
+
+// ---- the whole file pre-hashed, then the reference's own upload loop ----------
+// waves over pool buffers are at most -n parts wide (5 at
+// qsfs's default), which keeps every wave below the GPU's break-even.  Here
+// the pre-hash does not use the pool at all: qsmd5_hash_read pulls each part's
+// bytes from the caller's File::ReadNoLoad (File.cpp:308-375) in column
+// windows through the library's own bounded pinned staging, so one call hashes
+// every queued part of the file as one GPU batch.  Each digest then rides on
+// its part into the reference's loop, unchanged: one pool buffer at a time
+// (Acquire blocks while this thread holds none), ReadNoLoad into it,
+// UploadMultipart with the stored digest (QSTransferManager.cpp:602-673).
+
+struct StagedOptions {
+  uint64_t staging_bytes = 0;  // qsmd5_hash_read's budget (0: QSMD5_READ_STAGING_BYTES, 256 MiB)
+  size_t wave_parts = 0;       // parts per pre-hash call (0: every part of the file at once)
+  bool pipeline = true;        // pre-hash the next wave on a helper thread while this one uploads
+  bool upload_releases = false;  // as PrehashOptions::upload_releases
+  int flags = 0;               // qsmd5_hash_read flags (QSMD5_FLAG_GPU_ONLY / _CPU_ONLY)
+  std::function<bool()> should_continue;  // as PrehashOptions::should_continue (thread-safe)
+};
+
+namespace detail {
+
+// read_range(file_offset, len, char* dst) -> bytes copied (File::ReadNoLoad(...).first).
+template <class ReadRange>
+struct RangeReader {
+  const std::vector<qsmd5_part>* parts;
+  size_t first;
+  ReadRange* read;
+  std::exception_ptr err;
+  static uint64_t thunk(void* user, size_t chunk, uint64_t offset, uint64_t len, void* dst) {
+    RangeReader* r = static_cast<RangeReader*>(user);
+    if (r->err) return 0;
+    try {
+      const qsmd5_part& p = (*r->parts)[r->first + chunk];
+      return (uint64_t)(*r->read)(p.offset + offset, (size_t)len, static_cast<char*>(dst));
+    } catch (...) {  // never through the C library: carried out below
+      r->err = std::current_exception();
+      return 0;
+    }
+  }
+};
+
+struct StagedWave {
+  size_t first = 0, count = 0;
+  bool cancelled = false;
+  std::vector<uint8_t> dig;
+  int backend = 0;
+  double hash_s = 0;
+};
+
+template <class ReadRange>
+StagedWave prehash_wave(const std::vector<qsmd5_part>& parts, size_t first, size_t count,
+                        ReadRange& read_range, const StagedOptions& opt) {
+  StagedWave w;
+  w.first = first;
+  if (opt.should_continue && !opt.should_continue()) {
+    w.cancelled = true;
+    return w;
+  }
+  w.count = count;
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint64_t> lens(count);
+  for (size_t k = 0; k < count; ++k) lens[k] = parts[first + k].size;
+  w.dig.resize(16 * count);
+  RangeReader<ReadRange> rr{&parts, first, &read_range, nullptr};
+  const int rc = qsmd5_hash_read(lens.data(), count, &RangeReader<ReadRange>::thunk, &rr, opt.staging_bytes,
+                                 reinterpret_cast<uint8_t(*)[16]>(w.dig.data()), opt.flags);
+  if (rr.err) std::rethrow_exception(rr.err);
+  check(rc, "qsmd5_hash_read");
+  w.backend = qsmd5_last_backend();  // this thread's call
+  w.hash_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return w;
+}
+
+}  // namespace detail
+
+// Digests of every part, pulled through read_range in bounded staging (no pool
+// buffer used): hex text in part order.
+template <class ReadRange>
+std::vector<std::string> md5_parts_read(const std::vector<qsmd5_part>& parts, ReadRange&& read_range,
+                                        uint64_t staging_bytes = 0, int flags = 0) {
+  StagedOptions opt;
+  opt.staging_bytes = staging_bytes;
+  opt.flags = flags;
+  const detail::StagedWave w = detail::prehash_wave(parts, 0, parts.size(), read_range, opt);
+  std::vector<std::string> out(parts.size());
+  for (size_t k = 0; k < parts.size(); ++k) out[k] = detail::hex(&w.dig[16 * k]);
+  return out;
+}
+
+// parts, pool, upload: as upload_parts_prehashed.  read_range(file_offset,
+// len, char* dst) -> bytes copied: File::ReadNoLoad(off, len, dst).first; with
+// `pipeline` it is also called from the helper thread pre-hashing the next
+// wave, so it must be thread-safe (ReadNoLoad locks the file).  Stats: waves =
+// pre-hash calls, gpu_waves / cpu_waves by their backend, hash_s = time in
+// them (reads included), upload_s = the upload loop (its own reads included),
+// wait_s = upload time spent waiting for a pre-hash (hashing not hidden).
+// A short read or a hashing failure throws before any part of that wave is
+// uploaded; the pool is never held by the pre-hash.
+template <class Pool, class ReadRange, class Upload>
+WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, ReadRange&& read_range,
+                              Upload&& upload, const StagedOptions& opt = StagedOptions()) {
+  using clock = std::chrono::steady_clock;
+  auto secs = [](clock::time_point a, clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+  };
+  WaveStats st;
+  const auto t_start = clock::now();
+  if (parts.empty()) return st;
+  const size_t per = opt.wave_parts ? opt.wave_parts : parts.size();
+  auto prep = [&](size_t first) {
+    return detail::prehash_wave(parts, first, std::min(per, parts.size() - first), read_range, opt);
+  };
+  std::future<detail::StagedWave> ahead;
+  auto drain_ahead = [&]() noexcept {
+    if (!ahead.valid()) return;
+    try {
+      (void)ahead.get();
+    } catch (...) {
+    }
+  };
+  auto stop_requested = [&] { return opt.should_continue && !opt.should_continue(); };
+  const auto tw = clock::now();
+  detail::StagedWave cur = prep(0);
+  st.wait_s += secs(tw, clock::now());
+  for (;;) {
+    if (cur.cancelled) {
+      st.stopped = true;
+      break;
+    }
+    const size_t n = cur.count, next = cur.first + n;
+    ++st.waves;
+    st.parts += n;
+    st.widest_wave = std::max(st.widest_wave, n);
+    st.hash_s += cur.hash_s;
+    switch (cur.backend) {
+      case QSMD5_BACKEND_GPU: ++st.gpu_waves; break;
+      case QSMD5_BACKEND_SPLIT: ++st.split_waves; break;
+      default: ++st.cpu_waves; break;
+    }
+    if (opt.pipeline && next < parts.size()) {
+      try {
+        ahead = std::async(std::launch::async, prep, next);
+      } catch (...) {
+        // no thread or no memory for one: the next wave is pre-hashed here, after this one
+      }
+    }
+    const auto t0 = clock::now();
+    size_t k = 0;
+    try {
+      for (; k < n; ++k) {
+        if (stop_requested()) break;
+        const qsmd5_part& p = parts[cur.first + k];
+        // The reference's loop body (QSTransferManager.cpp:609-665): one
+        // buffer, acquired while this thread holds none.
+        typename Pool::buffer_type b = pool.acquire();
+        if (!Pool::data(b)) throw std::runtime_error("transfer buffer pool is shut down: upload stopped");
+        try {
+          if (Pool::size(b) < p.size) throw std::invalid_argument("pool buffer smaller than a part");
+          const size_t got = read_range(p.offset, (size_t)p.size, Pool::data(b));
+          if (got != p.size)
+            throw std::runtime_error("short read of part " + std::to_string(p.part_number) + ": " +
+                                     std::to_string(got) + " of " + std::to_string(p.size) + " bytes");
+          upload(p, b, detail::hex(&cur.dig[16 * k]));
+        } catch (...) {
+          pool.release(b);  // not handed over
+          throw;
+        }
+        if (!opt.upload_releases) pool.release(b);  // ReceivedHandlerMultipleUpload
+        ++st.uploaded;
+      }
+    } catch (...) {
+      drain_ahead();
+      throw;
+    }
+    st.upload_s += secs(t0, clock::now());
+    if (k < n) {
+      drain_ahead();
+      st.stopped = true;
+      break;
+    }
+    if (next >= parts.size()) break;
+    const auto t1 = clock::now();
+    cur = ahead.valid() ? ahead.get() : prep(next);
+    st.wait_s += secs(t1, clock::now());
   }
   st.wall_s = secs(t_start, clock::now());
   return st;

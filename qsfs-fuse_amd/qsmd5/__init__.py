@@ -22,7 +22,7 @@ import os
 __all__ = [
     "Md5Error", "lib", "lib_path", "shutdown", "hexdigest", "md5", "md5_stream", "MD5", "hash_batch",
     "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
-    "alloc_pinned", "free_pinned", "register_host", "unregister_host", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
+    "alloc_pinned", "free_pinned", "hash_read", "buffer_reader", "register_host", "unregister_host", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
     "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST", "FLAG_GPU_ONLY",
     "FLAG_CPU_ONLY", "stats", "rates", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU", "BACKEND_SPLIT",
 ]
@@ -80,6 +80,10 @@ class Part(ctypes.Structure):
 
 
 _lib = None
+
+# qsmd5_read_fn: uint64_t (*)(void* user, size_t chunk, uint64_t offset, uint64_t len, void* dst)
+READ_FN = ctypes.CFUNCTYPE(ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
+                           ctypes.c_uint64, ctypes.c_void_p)
 
 # qsmd5_log_fn: void (*)(int level, const char* msg, void* user)
 LOG_FN = ctypes.CFUNCTYPE(None, ctypes.c_int, ctypes.c_char_p, ctypes.c_void_p)
@@ -155,6 +159,8 @@ def lib():
                                                 ctypes.c_uint32, ctypes.c_uint32,
                                                 ctypes.c_void_p]),
         "qsmd5_set_log_callback": (ctypes.c_int, [LOG_FN, ctypes.c_void_p]),
+        "qsmd5_hash_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t, READ_FN,
+                                           ctypes.c_void_p, ctypes.c_uint64, c_u8p, ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -377,6 +383,50 @@ def hash_parts(file_buf, parts):
     _check(lib().qsmd5_hash_parts(p, arr, n, out), "qsmd5_hash_parts")
     raw = bytes(out)
     return [raw[16 * i:16 * i + 16] for i in range(n)]
+
+
+def hash_read(lens, read, staging_bytes=0, flags=0):
+    """qsmd5_hash_read: MD5 of n chunks the library pulls in column windows
+    through ``read(chunk, offset, length, dst_address) -> bytes copied`` (the
+    File::ReadNoLoad form), staging at most ``staging_bytes`` (0: default).
+    Returns the list of 16-byte digests.  An exception in ``read`` fails the
+    call and is re-raised here."""
+    lens = [int(x) for x in lens]
+    n = len(lens)
+    if n == 0:
+        return []
+    arr = (ctypes.c_uint64 * n)(*lens)
+    errors = []
+
+    def thunk(_user, chunk, offset, length, dst):
+        if errors:
+            return 0
+        try:
+            return int(read(chunk, offset, length, dst))
+        except BaseException as e:  # noqa: B902 -- carried to the caller below
+            errors.append(e)
+            return 0  # a short read: the library stops and returns -EIO
+
+    cb = READ_FN(thunk)  # alive for the whole call: the library calls it only inside it
+    out = (ctypes.c_uint8 * (16 * n))()
+    rc = lib().qsmd5_hash_read(arr, n, cb, None, staging_bytes, out, flags)
+    if errors:
+        raise errors[0]
+    _check(rc, "qsmd5_hash_read")
+    raw = bytes(out)
+    return [raw[16 * i:16 * i + 16] for i in range(n)]
+
+
+def buffer_reader(chunks):
+    """A read callback over in-memory chunks [(address, length), ...]: copies
+    the asked window with ctypes.memmove."""
+    def read(chunk, offset, length, dst):
+        addr, L = chunks[chunk]
+        if offset + length > L:
+            return 0
+        ctypes.memmove(dst, addr + offset, length)
+        return length
+    return read
 
 
 class MD5(object):

@@ -25,7 +25,7 @@ for v in tsan asan; do
   HOSTSAN=""
   for f in $SAN; do HOSTSAN="$HOSTSAN -Xarch_host $f"; done
   RT_OBJS=""
-  for u in qsmd5_runtime qsmd5_rt_device qsmd5_rt_staging qsmd5_rt_route; do
+  for u in qsmd5_runtime qsmd5_rt_device qsmd5_rt_staging qsmd5_rt_route qsmd5_rt_read; do
     $HIPCC -O1 -g -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function $HOSTSAN \
       -x hip -c "$R/qsfs-fuse_amd/csrc/$u.cpp" -o "$OUT/${u}_$v.o"
     RT_OBJS="$RT_OBJS $OUT/${u}_$v.o"

@@ -24,6 +24,10 @@
 // with status 3.  --naive-wave=W replaces the helper with the hold-and-wait
 // flow round 3's INTEGRATION.md sketched (W blocking Acquire calls before the
 // wave is hashed): the negative control that deadlocks under the same load.
+// --staged replaces the waves with the pool-free pre-hash:
+// qsmd5::upload_parts_staged pulls every part through qsmd5_hash_read in column
+// windows (--staging=BYTES budget, --wave-parts=W parts per call, default the
+// whole file), then runs the reference's loop one pool buffer at a time.
 // File content: part-aligned mode (--aligned) makes part i = LCG(12345 + i),
 // the parts of tests/golden/batch_10MiB.json, for every file; otherwise file f
 // is one LCG(seed + f) stream.  Prints one JSON object with the digests in
@@ -309,7 +313,9 @@ qsmd5::WaveStats naive_upload(const std::vector<qsmd5_part>& parts, WatchedPool&
 int main(int argc, char** argv) {
   uint64_t size = 64ull * 10 * 1024 * 1024;
   size_t pool_n = 5, files = 1, naive_wave = 0, max_wave = 0;
-  bool aligned = false, pinned = false, slab = false, reg = false, pipeline = true;
+  bool aligned = false, pinned = false, slab = false, reg = false, pipeline = true, staged = false;
+  uint64_t staging = 0;
+  size_t wave_parts = 0;
   uint32_t seed = 12345;
   uint64_t buf = 10ull << 20;
   int repeat = 1, async_threads = 0;
@@ -335,6 +341,9 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--fail-upload-part=")) fail_upload_part = (uint32_t)strtoul(v, nullptr, 0);
     else if (const char* v = val("--cancel-after=")) cancel_after = strtoull(v, nullptr, 0);
     else if (const char* v = val("--check-throws-after=")) check_throws_after = strtoull(v, nullptr, 0);
+    else if (const char* v = val("--staging=")) staging = strtoull(v, nullptr, 0);
+    else if (const char* v = val("--wave-parts=")) wave_parts = strtoull(v, nullptr, 0);
+    else if (a == "--staged") staged = true;
     else if (a == "--aligned") aligned = true;
     else if (a == "--pinned") pinned = true;
     else if (a == "--slab") slab = true;
@@ -476,8 +485,28 @@ int main(int argc, char** argv) {
               inflight.done();
             });
           };
+          // --staged: File::ReadNoLoad over any byte range of the file (the short-read
+          // fault hits any window inside the chosen part)
+          auto read_range = [&](uint64_t off, size_t len, char* dst) {
+            const size_t got = pf.read(off, len, dst);
+            if (short_read_part) {
+              const qsmd5_part& sp = parts[short_read_part - 1];
+              if (off >= sp.offset && off < sp.offset + sp.size) return got / 2;
+            }
+            return got;
+          };
           try {
-            st[f] = qsmd5::upload_parts_prehashed(parts, shared, read, upload, opt);
+            if (staged) {
+              qsmd5::StagedOptions so;
+              so.staging_bytes = staging;
+              so.wave_parts = wave_parts;
+              so.pipeline = pipeline;
+              so.upload_releases = opt.upload_releases;
+              so.should_continue = opt.should_continue;
+              st[f] = qsmd5::upload_parts_staged(parts, shared, read_range, upload, so);
+            } else {
+              st[f] = qsmd5::upload_parts_prehashed(parts, shared, read, upload, opt);
+            }
           } catch (...) {
             inflight.wait();  // parts handed over before the failure are still uploading
             throw;
@@ -540,14 +569,14 @@ int main(int argc, char** argv) {
     return s + "]";
   };
   printf("{\"deadlock\": false, \"error\": \"%s\", \"uploaded\": %zu, \"stats_uploaded\": %zu, \"stopped\": %zu, \"pool_free_after\": %zu, \"size\": %llu, \"parts\": %zu, \"files\": %zu, \"pages\": %zu, \"pool\": %zu, "
-         "\"pinned\": %s, \"slab\": %s, \"registered\": %s, \"pipeline\": %s, \"async_threads\": %d, "
+         "\"pinned\": %s, \"slab\": %s, \"registered\": %s, \"pipeline\": %s, \"staged\": %s, \"staging\": %llu, \"async_threads\": %d, "
          "\"naive_wave\": %zu, \"upload_ms\": %.3f, \"register_s\": %.6f, \"waves\": %zu, "
          "\"widest_wave\": %zu, \"gpu_waves\": %zu, \"cpu_waves\": %zu, \"split_waves\": %zu, "
          "\"seconds\": %.6f, \"gather_s\": %.6f, \"hash_s\": %.6f, \"upload_s\": %.6f, \"wait_s\": %.6f, "
          "\"part_sizes\": [",
          errors[0].c_str(), uploaded, sum.uploaded, stopped, pool_free_after, (unsigned long long)size, n, files, file[0].pages.size(), pool_n, pinned ? "true" : "false",
          slab ? "true" : "false", reg && !pinned ? "true" : "false", pipeline ? "true" : "false",
-         async_threads, naive_wave, upload_ms, register_s, sum.waves, sum.widest_wave, sum.gpu_waves,
+         staged ? "true" : "false", (unsigned long long)staging, async_threads, naive_wave, upload_ms, register_s, sum.waves, sum.widest_wave, sum.gpu_waves,
          sum.cpu_waves, sum.split_waves, total, sum.gather_s, sum.hash_s, sum.upload_s, sum.wait_s);
   for (size_t i = 0; i < n; ++i) printf("%s%llu", i ? ", " : "", (unsigned long long)parts[i].size);
   printf("], \"hash_s_runs\": [");

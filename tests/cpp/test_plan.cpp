@@ -360,6 +360,88 @@ static int run_pipeline_cases(std::mt19937_64& rng) {
   return cases;
 }
 
+// Pull-driven batches (plan_read, qsmd5_hash_read): groups cover the lanes in
+// order; every byte of every chunk lies in exactly one column window; each
+// column's live lanes are a prefix and fit one region (count x stride); W is a
+// multiple of 64 (256 for the staged stride), at least kReadColMin unless one
+// column holds the group's longest chunk; a group never exceeds kReadMaxRows.
+static int check_read(const std::vector<uint64_t>& len, uint64_t staging, const char* what) {
+  const ReadPlan P = plan_read(len, staging);
+  if (len.empty()) {
+    CHECK(P.groups.empty(), "%s: empty input", what);
+    return 1;
+  }
+  size_t next = 0;
+  for (const ReadGroup& g : P.groups) {
+    CHECK(g.first == next && g.count > 0 && g.count <= kReadMaxRows, "%s: group range", what);
+    CHECK(g.W % 64 == 0 && g.W > 0, "%s: W %llu", what, (unsigned long long)g.W);
+    CHECK(g.stride == stage_bytes(g.W) && g.count * g.stride <= P.region, "%s: rows do not fit", what);
+    const uint64_t L0 = len[g.first];
+    CHECK(g.W >= kReadColMin || (uint64_t)g.ncols * g.W >= L0, "%s: narrow W", what);
+    CHECK((uint64_t)g.ncols * g.W >= L0 && (g.ncols == 1 || (uint64_t)(g.ncols - 1) * g.W < L0),
+          "%s: ncols", what);
+    for (uint32_t j = 0; j < g.ncols; ++j) {
+      const size_t a = ReadPlan::active(len, g, j);
+      CHECK(a >= 1 && a <= g.count, "%s: empty column %u", what, j);
+      for (size_t k = 0; k < g.count; ++k) {
+        const uint64_t b = ReadPlan::col_bytes(g, len[g.first + k], j);
+        CHECK((k < a) == (b > 0 || j == 0), "%s: live lanes not a prefix (col %u lane %zu)", what, j, k);
+      }
+    }
+    for (size_t k = 0; k < g.count; ++k) {  // the windows tile each chunk exactly
+      uint64_t sum = 0;
+      for (uint32_t j = 0; j < g.ncols; ++j) sum += ReadPlan::col_bytes(g, len[g.first + k], j);
+      CHECK(sum == len[g.first + k], "%s: lane %zu covered %llu of %llu bytes", what, g.first + k,
+            (unsigned long long)sum, (unsigned long long)len[g.first + k]);
+    }
+    next += g.count;
+  }
+  CHECK(next == len.size(), "%s: lanes not all grouped", what);
+  CHECK(P.region >= staging / 2 && (P.region <= staging / 2 || P.region == stage_bytes(kReadColMin)),
+        "%s: region", what);
+  return 1;
+}
+
+static int run_read_cases(std::mt19937_64& rng) {
+  const uint64_t KiB = 1024, MiB = 1ull << 20, GiB = 1ull << 30;
+  int cases = 0;
+  std::vector<std::vector<uint64_t>> sets = {
+      {}, {0}, {1}, {64}, {10 * MiB}, std::vector<uint64_t>(128, 10 * MiB),
+      std::vector<uint64_t>(512, 10 * MiB), std::vector<uint64_t>(10000, 10 * MiB),
+      std::vector<uint64_t>(65535, 10 * MiB), {3 * GiB, 1, 0, 0}};
+  {
+    std::vector<uint64_t> v(10, 10 * MiB);  // PrepareUpload's averaged tail pair
+    v.push_back(5 * MiB + 6172);
+    v.push_back(5 * MiB + 6173);
+    sets.push_back(v);
+  }
+  for (int t = 0; t < 30; ++t) {
+    std::vector<uint64_t> v(1 + rng() % 2000);
+    for (auto& L : v) L = rng() % (1 + (rng() % 3 == 0 ? 64 * MiB : 300 * KiB));
+    sets.push_back(v);
+  }
+  for (auto& v : sets) {
+    std::sort(v.begin(), v.end(), [](uint64_t a, uint64_t b) { return a > b; });
+    for (uint64_t staging : {(uint64_t)0, 1 * MiB, 64 * MiB, 256 * MiB, 1 * GiB, 8 * GiB})
+      cases += check_read(v, staging, "read plan");
+  }
+  {  // the shapes the design promises (qsmd5_hash_read)
+    std::vector<uint64_t> v(512, 10 * MiB);
+    const ReadPlan P = plan_read(v, 512 * MiB);  // 256 MiB regions: 512 rows of 508 KiB
+    CHECK(P.groups.size() == 1 && P.groups[0].ncols == 21 && P.groups[0].W == 519936,
+          "512 x 10 MiB through 512 MiB: %zu groups, %u columns of %llu", P.groups.size(),
+          P.groups.empty() ? 0 : P.groups[0].ncols,
+          (unsigned long long)(P.groups.empty() ? 0 : P.groups[0].W));
+    std::vector<uint64_t> w(10000, 10 * MiB);  // rows of 64 KiB + skew: 3840 per region
+    const ReadPlan Q = plan_read(w, 512 * MiB);
+    CHECK(Q.groups.size() == 3 && Q.groups[0].count == 3840 && Q.groups[2].count == 2320,
+          "10000 parts through 512 MiB: %zu groups of %zu", Q.groups.size(),
+          Q.groups.empty() ? (size_t)0 : Q.groups[0].count);
+    ++cases;
+  }
+  return cases;
+}
+
 int main() {
   const uint64_t MiB = 1ull << 20, GiB = 1ull << 30;
   std::mt19937_64 rng(1234);
@@ -431,6 +513,7 @@ int main() {
   }
   cases += run_copy_run_cases(rng);
   cases += run_pipeline_cases(rng);
+  cases += run_read_cases(rng);
   printf("plan %s %d cases\n", fails ? "FAIL" : "ok", cases);
   return fails ? 1 : 0;
 }

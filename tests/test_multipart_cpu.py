@@ -187,3 +187,68 @@ def test_cancel_stops_the_upload_and_returns_every_buffer(after, mode):
     assert r["stopped"] == (files if after < 20 else 0), r
     for m in r["md5_files"]:
         assert m[:want] == gold[:want] and not any(m[want:]), m
+
+
+# ---- the pool-free pre-hash (--staged) -------------------------
+
+@pytest.mark.parametrize("extra", [[], ["--no-pipeline"], ["--wave-parts=5"],
+                                   ["--wave-parts=5", "--async=3"], ["--staging=1000000"]])
+def test_staged_prehash_matches_golden(extra):
+    """qsmd5::upload_parts_staged: every part of a 24-part file pre-hashed by
+    qsmd5_hash_read straight from the pages (no pool buffer), then the
+    reference's one-buffer-at-a-time loop at qsfs's default -n 5.  Waves of 5
+    parts pipelined on the helper thread, the async executor, and a 1 MB
+    budget (rows of 64 KiB, many groups) give the same golden digests, and
+    every pool buffer comes back."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    r = run(["--aligned", "--size=%d" % (24 * 10 * MiB), "--pool=5", "--staged"] + extra, "cpu")
+    assert r["staged"] is True and r["parts"] == 24 and r["uploaded"] == 24
+    assert r["md5"] == gold[:24]
+    assert r["pool_free_after"] == 5
+    want_waves = 5 if "--wave-parts=5" in extra else 1
+    assert r["waves"] == want_waves and r["widest_wave"] == (5 if want_waves == 5 else 24)
+
+
+def test_staged_ragged_file_matches_oracle():
+    for size, seed in ((25 * MiB + 3, 41), (100 * MiB + 12345, 42)):
+        r = run(["--size=%d" % size, "--seed=%d" % seed, "--pool=2", "--staged",
+                 "--staging=%d" % (4 * MiB)], "cpu")
+        data = lcg_bytes(seed, size)
+        base, off, want = ctypes.addressof(data), 0, []
+        for L in r["part_sizes"]:
+            want.append((base + off, L))
+            off += L
+        assert r["md5"] == [d.hex() for d in md5_many(want)], size
+
+
+def test_staged_concurrent_files_share_a_blocking_pool():
+    """Four files flushing at once through one 5-buffer blocking pool: the
+    pre-hash holds no buffer and the upload loop holds one at a time while it
+    holds none, so there is no hold-and-wait to deadlock on."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    r = run(["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5", "--files=4", "--upload-ms=2",
+             "--deadlock-s=10", "--staged", "--wave-parts=4", "--async=3"], "cpu", timeout=120)
+    assert r["deadlock"] is False
+    for f, got in enumerate(r["md5_files"]):
+        assert got == gold[:12], f
+
+
+@pytest.mark.parametrize("fault,upload_expected", [("--short-read-part=7", 0),
+                                                   ("--fail-upload-part=7", 6)])
+def test_staged_faults_stop_the_upload_and_return_every_buffer(fault, upload_expected):
+    """A short read inside part 7 fails the whole-file pre-hash before any
+    part is uploaded (the reference stops at its first short read,
+    QSTransferManager.cpp:625-643, after uploading the parts before it; here
+    no part goes out unhashed); a failing upload of part 7 stops after 6."""
+    out = run_raw(["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5", "--staged", fault], "cpu")
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    r = json.loads(out.stdout)
+    assert r["uploaded"] == upload_expected and r["pool_free_after"] == 5
+    assert ("short read" in r["error"]) == ("short-read" in fault)
+
+
+def test_staged_cancel_stops_between_parts():
+    r = run(["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5", "--staged", "--wave-parts=4",
+             "--cancel-after=6"], "cpu")
+    assert r["stopped"] == 1 and r["uploaded"] == 6 and r["stats_uploaded"] == 6
+    assert r["pool_free_after"] == 5

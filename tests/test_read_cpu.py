@@ -1,0 +1,144 @@
+"""qsmd5_hash_read -- the pull-driven batch behind the multipart pre-hash --
+on the library's CPU backend (no GPU needed).
+
+The library asks the caller's read(chunk, offset, length, dst) for each
+chunk's bytes in column windows (qsmd5_plan.h plan_read) and folds every
+window into that chunk's running MD5.  Checked here: digests against the
+reference-produced fixtures and the pinned oracle over every padding edge,
+empty chunks, groups and columns forced by a tiny staging budget; the read
+contract (each chunk's windows in increasing offset order, every byte asked
+for exactly once, nothing past the chunk); a short read fails the call with
+-EIO as the reference's upload stops (QSTransferManager.cpp:625-643); and
+the reader's exception reaches the caller.  The GPU path of the same entry
+point is tests/test_gpu_read.py.
+"""
+import ctypes
+import random
+
+import pytest
+
+import qsmd5
+from oracle_util import lcg_bytes, md5_many
+
+CPU = qsmd5.FLAG_CPU_ONLY
+MiB = 1 << 20
+
+
+class Recorder(object):
+    """A reader over in-memory buffers that records every call."""
+
+    def __init__(self, bufs, lens):
+        self.bufs, self.lens, self.calls = bufs, lens, []
+
+    def __call__(self, chunk, offset, length, dst):
+        self.calls.append((chunk, offset, length))
+        if offset + length > self.lens[chunk]:
+            return 0
+        ctypes.memmove(dst, ctypes.addressof(self.bufs[chunk]) + offset, length)
+        return length
+
+    def check_contract(self):
+        seen = {}
+        for c, off, length in self.calls:
+            assert length > 0
+            assert off == seen.get(c, 0), "chunk %d: window at %d, expected %d" % (c, off, seen.get(c, 0))
+            seen[c] = off + length
+        for c, L in enumerate(self.lens):
+            assert seen.get(c, 0) == L, "chunk %d: %d of %d bytes read" % (c, seen.get(c, 0), L)
+
+
+def _case(lens, staging, seed=7):
+    bufs = [lcg_bytes(seed + i, L) for i, L in enumerate(lens)]
+    rec = Recorder(bufs, lens)
+    got = qsmd5.hash_read(lens, rec, staging_bytes=staging, flags=CPU)
+    want = md5_many([(b, L) for b, L in zip(bufs, lens)])
+    assert got == want
+    rec.check_contract()
+    return rec
+
+
+def test_read_lcg_lengths_match_reference(golden):
+    """Every padding edge 0..200 B and the longer lengths of the fixture, each
+    the first L bytes of LCG(12345), through windows of a 1 MiB budget."""
+    g = golden("lcg_lengths.json")
+    cases = [c for c in g["cases"] if c["len"] <= 16 * MiB]
+    lens = [c["len"] for c in cases]
+    src = lcg_bytes(12345, max(lens))
+    rec = Recorder([src] * len(lens), lens)
+    got = qsmd5.hash_read(lens, rec, staging_bytes=1 * MiB, flags=CPU)
+    assert [d.hex() for d in got] == [c["md5"] for c in cases]
+    rec.check_contract()
+
+
+def test_read_file_parts_match_batch_fixture(golden):
+    """Parts of a file whose part i is LCG(12345 + i): the first 24 digests of
+    batch_10MiB.json, read through a 64 MiB budget (10 columns per part)."""
+    want = golden("batch_10MiB.json")["md5"][:24]
+    L = 10 * MiB
+    lens = [L] * 24
+    bufs = [lcg_bytes(12345 + i, L) for i in range(24)]
+    rec = Recorder(bufs, lens)
+    got = qsmd5.hash_read(lens, rec, staging_bytes=64 * MiB, flags=CPU)
+    assert [d.hex() for d in got] == want
+    rec.check_contract()
+
+
+@pytest.mark.parametrize("staging", [0, 1, 200000, 1 * MiB, 16 * MiB])
+def test_read_ragged_groups_and_columns(staging):
+    """Ragged lengths (empty, sub-block, block edges, multi-MiB) in caller
+    order unrelated to length; tiny budgets force many groups of few rows."""
+    rng = random.Random(staging + 3)
+    lens = [0, 1, 55, 56, 63, 64, 65, 119, 120, 128, 4096, 3 * MiB + 5, 0, 2 * MiB]
+    lens += [rng.randrange(0, 3 * MiB) for _ in range(40)]
+    rng.shuffle(lens)
+    _case(lens, staging)
+
+
+def test_read_short_read_fails_with_eio():
+    L = 3 * MiB
+    bufs = [lcg_bytes(1, L), lcg_bytes(2, L)]
+
+    def short(chunk, offset, length, dst):
+        ctypes.memmove(dst, ctypes.addressof(bufs[chunk]) + offset, length)
+        return length - 1 if chunk == 1 else length  # ReadNoLoad found a hole
+
+    with pytest.raises(qsmd5.Md5Error) as e:
+        qsmd5.hash_read([L, L], short, flags=CPU)
+    assert e.value.code == -5  # -EIO
+    assert "short read of chunk 1" in str(e.value)
+
+
+def test_read_reader_exception_reaches_the_caller():
+    def boom(chunk, offset, length, dst):
+        raise KeyError("page gone")
+
+    with pytest.raises(KeyError):
+        qsmd5.hash_read([100, 200], boom, flags=CPU)
+
+
+def test_read_argument_errors():
+    L = qsmd5.lib()
+    out = (ctypes.c_uint8 * 16)()
+    lens = (ctypes.c_uint64 * 1)(5)
+    assert L.qsmd5_hash_read(lens, 1, qsmd5.READ_FN(), None, 0, out, CPU) == -22  # NULL read
+    assert L.qsmd5_hash_read(lens, 0, qsmd5.READ_FN(), None, 0, out, CPU) == 0    # nothing to do
+    big = (ctypes.c_uint64 * 1)(1 << 38)
+    assert L.qsmd5_hash_read(big, 1, qsmd5.READ_FN(lambda *a: 0), None, 0, out, CPU) == -22
+    assert L.qsmd5_hash_read(lens, 1, qsmd5.READ_FN(lambda *a: 0), None, 0, out,
+                             qsmd5.FLAG_CPU_ONLY | qsmd5.FLAG_GPU_ONLY) == -22
+
+
+def test_read_auto_mode_without_gpu_falls_back(monkeypatch):
+    """QSMD5_BACKEND=auto on a box without a GPU: a file of 64 x 1 MiB parts
+    prices to the GPU, whose initialisation fails; the batch is read again from
+    the start and hashed on the CPU, same digests."""
+    if qsmd5.device_count() > 0:
+        pytest.skip("a GPU is present: the fallback is exercised by the GPU suite")
+    monkeypatch.setenv("QSMD5_BACKEND", "auto")
+    monkeypatch.setenv("QSMD5_GPU_CHAIN_GIBS", "100")  # price the GPU as the faster
+    lens = [1 * MiB] * 64
+    bufs = [lcg_bytes(900 + i, L) for i, L in enumerate(lens)]
+    rec = Recorder(bufs, lens)
+    got = qsmd5.hash_read(lens, rec)
+    assert got == md5_many([(b, L) for b, L in zip(bufs, lens)])
+    assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
