@@ -361,6 +361,16 @@ typedef struct qsmd5_rates {
 } qsmd5_rates;
 QSMD5_API int qsmd5_get_rates(qsmd5_rates* out);
 
+/* The share of its priced rate the CPU backend got in its recent batches
+ * (1.0 = as priced on an idle host; 0.5 = its batches took twice the
+ * estimate: the host's cores are busy with other work).  Every CPU batch
+ * priced at >= 2 ms is timed; a new sample weighs 1/2, and the value relaxes
+ * back to 1 with a 10 s time constant (QSMD5_CPU_EFF_DECAY_S) when no CPU
+ * batch runs.  QSMD5_BACKEND=auto divides its CPU estimates by it, so a busy
+ * host sends batches to the GPU earlier (QSMD5_CPU_LOAD_FEEDBACK=0: always
+ * 1).  Host-only, needs no GPU. */
+QSMD5_API int qsmd5_get_cpu_efficiency(double* out);
+
 /* Process-wide backend counters since load. */
 typedef struct qsmd5_stats {
   uint64_t gpu_batches;  /* calls hashed by the gfx950 kernels */

@@ -485,14 +485,28 @@ struct DeviceRestore {
 // for it, then initialise afresh.  A child forked after init takes no lock: a
 // parent thread may have held it at fork(), and the child never touches the
 // parent's HIP state anyway.
+//
+// glibc's rwlock prefers readers: while any call holds g_calls shared, a new
+// lock_shared succeeds even with shutdown waiting for the exclusive lock, so
+// calls that keep overlapping (executor + FUSE threads) could starve shutdown
+// forever (tests/cpp/shutdown_starvation.cpp: 20 s and counting
+// before this gate).  So a shutdown first raises g_shutdown_pending, and a new
+// OUTERMOST call waits at the gate until no shutdown is pending; calls
+// already in flight finish, and the exclusive lock comes free.
 extern std::shared_mutex g_calls;
 extern thread_local int t_call_depth;
-
+extern std::atomic<int> g_shutdown_pending;  // shutdowns waiting for or holding g_calls
+extern std::mutex g_gate_mu;
+extern std::condition_variable g_gate_cv;
 
 struct CallScope {
   bool locked = false;
   CallScope() {
     if (t_call_depth++ == 0 && !g_forked_child.load(std::memory_order_relaxed)) {
+      if (g_shutdown_pending.load(std::memory_order_acquire) > 0) {
+        std::unique_lock<std::mutex> lk(g_gate_mu);
+        g_gate_cv.wait(lk, [] { return g_shutdown_pending.load() == 0; });
+      }
       g_calls.lock_shared();
       locked = true;
     }
@@ -551,6 +565,12 @@ double link_gibs();
 double gpu_est_ms(uint64_t longest, uint64_t host_bytes);
 double gpu_wait_est_ms(uint64_t longest, uint64_t host_bytes);  // its lower bound, for sleeping
 double cpu_est_ms(uint64_t longest, uint64_t total, uint64_t d2h_bytes = 0);
+// Load feedback (qsmd5_rt_route.cpp): the share of its priced rate the CPU
+// backend got lately (1 = as priced); note_cpu_batch adds a timed batch.
+double cpu_efficiency();
+void note_cpu_batch(double priced_ms, double measured_ms);
+double cpu_priced_ms(const qsmd5_chunk* chunks, size_t n, int flags);
+double cpu_model_ms(uint64_t longest, uint64_t total);  // scalar chains, idle host
 bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags);
 std::vector<uint32_t> plan_split(const qsmd5_chunk* chunks, size_t n, int flags);
 int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags,

@@ -143,7 +143,7 @@ int gpu_read(Dev& r, ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
 // The CPU backend of a pull-driven batch: the same windows into a host buffer,
 // each window's rows folded into their chunks' running contexts (md5_cpu.h
 // Ctx) on up to cpu_threads() threads.
-int cpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
+int cpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16], double* hash_ms) {
   const size_t n = J.len.size();
   const ReadPlan P = plan_read(J.sorted, staging);
   uint64_t region = 0;
@@ -155,6 +155,7 @@ int cpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
     for (uint32_t j = 0; j < g.ncols; ++j) {
       const size_t act = ReadPlan::active(J.sorted, g, j);
       if (int rc = fill_window(J, g, j, act, buf.get())) return rc;
+      const auto t0 = std::chrono::steady_clock::now();  // the hashing, not the reads
       std::atomic<size_t> next{0};
       auto work = [&]() noexcept {
         for (size_t k; (k = next.fetch_add(1)) < act;) {
@@ -174,6 +175,7 @@ int cpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
       }
       work();
       for (auto& t : th) t.join();
+      *hash_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
   for (size_t c = 0; c < n; ++c) ctx[c].final(digests[c]);
   return 0;
@@ -217,11 +219,13 @@ int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* u
                                          : env_u64("QSMD5_READ_STAGING_BYTES", kDefaultReadStaging);
   auto on_cpu = [&](const char* reason) {
     log_read("cpu", reason, J);
-    const int rc = cpu_read(J, staging, digests);
+    double hash_ms = 0;
+    const int rc = cpu_read(J, staging, digests, &hash_ms);
     if (rc == 0) {
       t_last_backend = QSMD5_BACKEND_CPU;
       g_cpu_batches.fetch_add(1);
       g_cpu_chunks.fetch_add(n);
+      note_cpu_batch(cpu_model_ms(longest, J.total), hash_ms);  // scalar chains, as cpu_read runs them
     }
     return rc;
   };

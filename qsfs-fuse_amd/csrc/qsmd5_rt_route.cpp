@@ -1,6 +1,8 @@
 // qsfs-fuse_amd/csrc/qsmd5_rt_route.cpp -- group commit of concurrent callers, backend
 // routing and its cost model, the CPU backend, split batches, GPU-failure fallback
 // (the runtime's units: qsmd5_rt.h).
+#include <cmath>
+
 #include "qsmd5_rt.h"
 
 namespace qsmd5 {
@@ -9,6 +11,9 @@ namespace rt {
 // Calls in flight against qsmd5_shutdown: CallScope (qsmd5_rt.h).
 std::shared_mutex g_calls;
 thread_local int t_call_depth = 0;
+std::atomic<int> g_shutdown_pending{0};
+std::mutex g_gate_mu;
+std::condition_variable g_gate_cv;
 
 // ---- group commit ------------------------------------------------------------
 // qsfs hashes parts from up to numtransfer executor threads at once
@@ -375,25 +380,74 @@ double gpu_wait_est_ms(uint64_t longest, uint64_t host_bytes) {
   const double chain = std::max(gpu_chain_gibs(), kGpuChainGiBs);
   return 1e3 * ((double)longest / chain + (double)host_bytes / link_gibs()) / kGiB;
 }
-double cpu_est_ms(uint64_t longest, uint64_t total, uint64_t d2h_bytes) {
+// ---- the CPU backend under load --------------------------
+// The CPU estimates assume that each of the T backend threads gets a core.  A
+// qsfs daemon's own workers and FUSE threads (or other tenants) may hold those
+// cores; then a CPU batch takes longer than priced, and the GPU -- which
+// leaves the cores alone -- becomes the faster route.  So every CPU batch
+// priced at >= 2 ms is timed, and efficiency = priced / measured (at most 1)
+// is folded into an average (a new sample weighs 1/2); the CPU estimates are
+// divided by it.  Without a new sample it relaxes back to 1 with a 10 s time
+// constant (QSMD5_CPU_EFF_DECAY_S), so a load that has gone does not keep
+// batches off the CPU for good: the next CPU batch measures again.
+// QSMD5_CPU_LOAD_FEEDBACK=0 prices the idle host always; qsmd5_get_cpu_efficiency
+// reports the current value.
+static std::atomic<uint64_t> g_cpu_eff_bits{0};  // double; 0 = no sample yet
+static std::atomic<int64_t> g_cpu_eff_at{0};     // steady_clock ns of the last sample
+
+static int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+double cpu_efficiency() {
+  if (!env_u64("QSMD5_CPU_LOAD_FEEDBACK", 1)) return 1.0;
+  const uint64_t bits = g_cpu_eff_bits.load(std::memory_order_relaxed);
+  if (!bits) return 1.0;
+  double e;
+  memcpy(&e, &bits, sizeof(e));
+  const double tau = std::max<double>(0.001, (double)env_u64("QSMD5_CPU_EFF_DECAY_S", 10));
+  const double dt = std::max<double>(0.0, (now_ns() - g_cpu_eff_at.load(std::memory_order_relaxed)) * 1e-9);
+  return 1.0 - (1.0 - e) * std::exp(-dt / tau);
+}
+
+void note_cpu_batch(double priced_ms, double measured_ms) {
+  if (priced_ms < 2.0 || measured_ms <= 0) return;
+  const double sample = std::min(1.0, std::max(0.02, priced_ms / measured_ms));
+  const double cur = cpu_efficiency();
+  const double e = g_cpu_eff_bits.load(std::memory_order_relaxed) ? 0.5 * cur + 0.5 * sample : sample;
+  uint64_t bits;
+  memcpy(&bits, &e, sizeof(bits));
+  g_cpu_eff_bits.store(bits, std::memory_order_relaxed);
+  g_cpu_eff_at.store(now_ns(), std::memory_order_relaxed);
+}
+
+// The idle-host model (no load factor): the longest chain on one thread, or all
+// bytes over T threads.
+double cpu_model_ms(uint64_t longest, uint64_t total) {
   const double T = (double)cpu_threads(), rc = cpu_gibs_per_thread();
-  return 1e3 * (std::max((double)longest / rc, (double)total / (T * rc)) + (double)d2h_bytes / kD2HGiBs) / kGiB;
+  return 1e3 * std::max((double)longest / rc, (double)total / (T * rc)) / kGiB;
+}
+
+double cpu_est_ms(uint64_t longest, uint64_t total, uint64_t d2h_bytes) {
+  return cpu_model_ms(longest, total) / cpu_efficiency() + 1e3 * (double)d2h_bytes / kD2HGiBs / kGiB;
 }
 
 static uint64_t routed_len(const qsmd5_chunk& c, int flags) {
   return (flags & QSMD5_FLAG_REF_TRUNCATE32) ? (c.len & 0xffffffffull) : c.len;
 }
 
-// Opt-in (QSMD5_ROUTE_LANES=1): price the CPU backend's multi-buffer lanes
-// (cpu_batch, md5_cpu_mb.cpp) for batches that will run on them -- AVX-512F,
-// at least 2 chunks per thread, every chunk in host memory -- at this host's
-// measured 16-lane rate (a lane's chain = 1/16 of it).  Off by default (DESIGN.md
-// §1): the lanes are faster than the GPU below ~240 parts of 10 MiB at T = 4
-// on the MI355X box's EPYC 9575F (6.9 GiB/s per thread), but they hold T cores
-// at full AVX-512 load for the batch, and a qsfs daemon runs its transfer
-// workers and FUSE threads on those cores; the GPU leaves them free.
+// Price the CPU backend's multi-buffer lanes (cpu_batch, md5_cpu_mb.cpp) for
+// batches that will run on them -- AVX-512F, at least 2 chunks per thread,
+// every chunk in host memory -- at this host's measured 16-lane rate (a lane's
+// chain = 1/16 of it).  On by default since round 5: on the
+// MI355X box's EPYC 9575F the lanes beat a pool-bound GPU wave by ~3x up to
+// ~240 parts of 10 MiB on an idle host, and when qsfs's own
+// threads hold those cores the load feedback above (cpu_efficiency) sees the
+// lanes slow down and moves the batches to the GPU.  QSMD5_ROUTE_LANES=0
+// prices the scalar chains only (the round 1-4 default).
 static bool lanes_priced(const qsmd5_chunk* chunks, size_t n, int flags) {
-  if (!env_u64("QSMD5_ROUTE_LANES", 0) || !env_u64("QSMD5_CPU_MB", 1) ||
+  if (!env_u64("QSMD5_ROUTE_LANES", 1) || !env_u64("QSMD5_CPU_MB", 1) ||
       !qsmd5::cpu::mb16_available() || n < 2 * std::min<size_t>(cpu_threads(), n) ||
       cpu_rates().lane_thread <= 0)
     return false;
@@ -404,6 +458,15 @@ static bool lanes_priced(const qsmd5_chunk* chunks, size_t n, int flags) {
     if (chunks[i].len && cls(chunks[i].ptr, &owner) == kDeviceMem) return false;
   }
   return true;
+}
+
+// The lanes' idle-host model: the longest chain in one lane, or all bytes over
+// T threads' lanes together.
+static double lanes_model_ms(uint64_t longest, uint64_t total) {
+  const double lt = cpu_rates().lane_thread;  // a lane's chain: 1/(16 x groups) of it
+  const double lanes_per_thread = 16.0 * cpu_rates().mb_groups;
+  return 1e3 * std::max((double)longest / (lt / lanes_per_thread),
+                        (double)total / ((double)cpu_threads() * lt)) / kGiB;
 }
 
 // True when the CPU is expected to finish this batch first (see above).  The
@@ -421,10 +484,7 @@ bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
   const bool lanes = lanes_priced(chunks, n, flags);  // only for all-host batches
   auto cpu_ms_of = [&](uint64_t d2h) {
     if (!lanes) return cpu_est_ms(longest, total, d2h);
-    const double lt = cpu_rates().lane_thread;  // a lane's chain: 1/(16 x groups) of it
-    const double lanes_per_thread = 16.0 * cpu_rates().mb_groups;
-    return 1e3 * std::max((double)longest / (lt / lanes_per_thread),
-                          (double)total / ((double)cpu_threads() * lt)) / kGiB;
+    return lanes_model_ms(longest, total) / cpu_efficiency();
   };
   if (!(cpu_ms_of(0) < gpu_est_ms(longest, total))) return false;
   if (lanes || (flags & QSMD5_FLAG_HOST) || qsmd5_device_count() <= 0) return true;
@@ -436,6 +496,29 @@ bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
     if (L && cls(chunks[i].ptr, &owner) == kDeviceMem) dev_bytes += L;
   }
   return cpu_ms_of(dev_bytes) < gpu_est_ms(longest, total - dev_bytes);
+}
+
+// What the idle-host model prices a CPU batch of these (host) chunks at, for
+// the load feedback: the lanes where cpu_batch will run them, else scalar
+// chains.  Batches under 1 MiB are not worth a sample (0).
+double cpu_priced_ms(const qsmd5_chunk* chunks, size_t n, int flags) {
+  uint64_t total = 0, longest = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t L = routed_len(chunks[i], flags);
+    total += L;
+    longest = std::max(longest, L);
+  }
+  if (total < (1u << 20)) return 0.0;
+  if (!(flags & QSMD5_FLAG_HOST) && qsmd5_device_count() > 0) {  // device chunks: D2H-bound, no sample
+    Classifier cls(flags, n);
+    for (size_t i = 0; i < n; ++i) {
+      int owner = -1;
+      if (chunks[i].len && cls(chunks[i].ptr, &owner) == kDeviceMem) return 0.0;
+    }
+  }
+  const bool mb = env_u64("QSMD5_CPU_MB", 1) && qsmd5::cpu::mb16_available() &&
+                  cpu_rates().lane_thread > 0 && n >= 2 * std::min<size_t>(cpu_threads(), n);
+  return mb ? lanes_model_ms(longest, total) : cpu_model_ms(longest, total);
 }
 
 // Ragged batches (qsfs -b sweeps, a file's parts plus small files): the GPU's
@@ -521,8 +604,8 @@ static bool mb_pull(void* ctx, uint32_t* out) {
 // first, taken from a shared counter).  With AVX-512 (QSMD5_CPU_MB=0: never)
 // and at least 2 host chunks per thread, each thread runs 16 host chunks at
 // once, one per vector lane (md5_cpu_mb.cpp): 7-10x the scalar rate per
-// thread (ubench/cpu_mb_rate.py).  The routing cost model above still prices
-// the scalar path, so a batch is never sent to the CPU on the strength of it.  A device-resident chunk is read through
+// thread (ubench/cpu_mb_rate.py); the routing cost model prices them
+// (lanes_priced, QSMD5_ROUTE_LANES=0: scalar chains only).  A device-resident chunk is read through
 // the thread's own 8 MiB host buffer, piece by piece, so a fallback over a large
 // device batch holds at most 8 MiB per thread of host memory; that needs a
 // working HIP context.
@@ -784,11 +867,14 @@ int hash_routed(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
   const int gflags = flags & ~(QSMD5_FLAG_GPU_ONLY | QSMD5_FLAG_CPU_ONLY);
   auto on_cpu = [&](const char* reason) {
     log_call("cpu", reason, n, chunks);
+    const auto t0 = std::chrono::steady_clock::now();
     const int rc = cpu_batch(chunks, n, digests, gflags);
     if (rc == 0) {
       t_last_backend = QSMD5_BACKEND_CPU;
       g_cpu_batches.fetch_add(1);
       g_cpu_chunks.fetch_add(n);
+      note_cpu_batch(cpu_priced_ms(chunks, n, gflags),
+                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
     }
     return rc;
   };

@@ -522,10 +522,15 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
     if (!(used & (1u << k))) continue;
     hipEvent_t t = nullptr;
     if (int rc = events.make(&t, hipEventDefault)) return drain(rc);
-    QS_HIP(hipEventRecord(t, r.compute[k]));
+    // from here on copies of the caller's buffers may be in flight: every
+    // failure drains before it returns
+    if (hipError_t e = hipEventRecord(t, r.compute[k]); e != hipSuccess)
+      return drain(hip_fail(e, "hipEventRecord"));
     tails.push_back(t);
   }
-  if (!first_kernel) QS_HIP(hipEventRecord(r.ev_last, s0));
+  if (!first_kernel)
+    if (hipError_t e = hipEventRecord(r.ev_last, s0); e != hipSuccess)
+      return drain(hip_fail(e, "hipEventRecord"));
   uint64_t longest_len = 0, host_bytes = 0;
   for (size_t i = 0; i < n; ++i) longest_len = std::max(longest_len, len[i]);
   for (uint64_t L : host_len) host_bytes += L;
@@ -547,7 +552,8 @@ int run_batch(Dev& r, const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16
       idle_us = std::min(500, idle_us * 2);
     }
   }
-  QS_HIP(hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0));
+  if (hipError_t e = hipMemcpyAsync(r.h_dig.p, d_dig, n * 16, hipMemcpyDeviceToHost, s0); e != hipSuccess)
+    return drain(hip_fail(e, "hipMemcpyAsync D2H"));
   // one stream (a single slice, or device chunks only): copy and kernel in
   // stream order, so the cost model's copy + chain is what is left to wait
   const double est_ms = tails.empty() ? gpu_wait_est_ms(longest_len, host_bytes) : 0.0;

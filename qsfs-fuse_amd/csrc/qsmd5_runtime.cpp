@@ -67,6 +67,21 @@ int qsmd5_shutdown(void) {
   if (t_call_depth > 0)
     return fail(-EINVAL, "qsmd5_shutdown: called from inside a qsmd5 call on this thread");
   try {
+    // New calls wait at the gate (CallScope) from here until this returns, so
+    // calls that keep overlapping cannot starve the exclusive lock below.
+    {
+      std::lock_guard<std::mutex> gl(g_gate_mu);
+      g_shutdown_pending.fetch_add(1);
+    }
+    struct Reopen {
+      ~Reopen() {
+        {
+          std::lock_guard<std::mutex> gl(g_gate_mu);
+          g_shutdown_pending.fetch_sub(1);
+        }
+        g_gate_cv.notify_all();
+      }
+    } reopen;
     std::unique_lock<std::shared_mutex> calls(g_calls);  // every call in flight has returned
     std::lock_guard<std::mutex> lk(g_init_mu);
     Runtime& r = rt();
@@ -423,6 +438,12 @@ int qsmd5_get_rates(qsmd5_rates* out) {
                   (env_gibs("QSMD5_GPU_CHAIN_GIBS") > 0 ? QSMD5_RATE_GPU_ENV : 0);
     return 0;
   });
+}
+
+int qsmd5_get_cpu_efficiency(double* out) {
+  if (!out) return fail(-EINVAL, "qsmd5: NULL out");
+  *out = cpu_efficiency();
+  return 0;
 }
 
 int qsmd5_get_stats(qsmd5_stats* out) {

@@ -24,7 +24,7 @@ __all__ = [
     "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
     "alloc_pinned", "free_pinned", "hash_read", "buffer_reader", "register_host", "unregister_host", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
     "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST", "FLAG_GPU_ONLY",
-    "FLAG_CPU_ONLY", "stats", "rates", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU", "BACKEND_SPLIT",
+    "FLAG_CPU_ONLY", "stats", "rates", "cpu_efficiency", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU", "BACKEND_SPLIT",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -159,6 +159,7 @@ def lib():
                                                 ctypes.c_uint32, ctypes.c_uint32,
                                                 ctypes.c_void_p]),
         "qsmd5_set_log_callback": (ctypes.c_int, [LOG_FN, ctypes.c_void_p]),
+        "qsmd5_get_cpu_efficiency": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double)]),
         "qsmd5_hash_read": (ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.c_size_t, READ_FN,
                                            ctypes.c_void_p, ctypes.c_uint64, c_u8p, ctypes.c_int]),
     }
@@ -234,6 +235,14 @@ def rates():
     r = Rates()
     _check(lib().qsmd5_get_rates(ctypes.byref(r)), "qsmd5_get_rates")
     return r.asdict()
+
+
+def cpu_efficiency():
+    """qsmd5_get_cpu_efficiency: the share of its priced rate the CPU backend
+    got lately (1.0 on an idle host); auto routing divides CPU estimates by it."""
+    v = ctypes.c_double()
+    _check(lib().qsmd5_get_cpu_efficiency(ctypes.byref(v)), "qsmd5_get_cpu_efficiency")
+    return v.value
 
 
 def route(lengths, flags=0):

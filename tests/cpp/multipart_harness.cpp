@@ -39,6 +39,7 @@
 #include <string.h>
 #include <dirent.h>
 #include <pthread.h>
+#include <sched.h>
 #include <sys/resource.h>
 #include <unistd.h>
 
@@ -316,6 +317,7 @@ int main(int argc, char** argv) {
   bool aligned = false, pinned = false, slab = false, reg = false, pipeline = true, staged = false;
   uint64_t staging = 0;
   size_t wave_parts = 0;
+  size_t cpus = 0, load_threads = 0;  // --cpus: the process's cores; --load: spinning threads on them
   uint32_t seed = 12345;
   uint64_t buf = 10ull << 20;
   int repeat = 1, async_threads = 0;
@@ -343,6 +345,8 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--check-throws-after=")) check_throws_after = strtoull(v, nullptr, 0);
     else if (const char* v = val("--staging=")) staging = strtoull(v, nullptr, 0);
     else if (const char* v = val("--wave-parts=")) wave_parts = strtoull(v, nullptr, 0);
+    else if (const char* v = val("--cpus=")) cpus = strtoull(v, nullptr, 0);
+    else if (const char* v = val("--load=")) load_threads = strtoull(v, nullptr, 0);
     else if (a == "--staged") staged = true;
     else if (a == "--aligned") aligned = true;
     else if (a == "--pinned") pinned = true;
@@ -357,6 +361,21 @@ int main(int argc, char** argv) {
   if (pool_n < 1) {
     fprintf(stderr, "--pool must be >= 1\n");
     return 2;
+  }
+  // --cpus=C: a daemon held to C cores (the first C of its allowed set), set
+  // before any thread -- the library's and HIP's included -- is created, so
+  // every thread inherits it.
+  if (cpus) {
+    cpu_set_t allowed, use;
+    CPU_ZERO(&use);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed)) return 1;
+    size_t taken = 0;
+    for (int c = 0; c < CPU_SETSIZE && taken < cpus; ++c)
+      if (CPU_ISSET(c, &allowed)) {
+        CPU_SET(c, &use);
+        ++taken;
+      }
+    if (sched_setaffinity(0, sizeof(use), &use)) return 1;
   }
   // The files' bytes, cut into pages of 1 KiB .. 3 MiB (aligned: one shared
   // file, every part golden; otherwise file f = LCG(seed + f)).
@@ -411,6 +430,21 @@ int main(int argc, char** argv) {
       }
     register_s = std::chrono::duration<double>(clock_type::now() - r0).count();
   }
+  // --load=K: K threads spinning on the process's cores for the whole run,
+  // standing in for qsfs's own transfer workers and FUSE threads.  The
+  // library's host rates are measured first, on the idle host, as a daemon's
+  // start-up would.
+  qsmd5_rates rates0;
+  (void)qsmd5_get_rates(&rates0);
+  std::atomic<bool> load_stop{false};
+  std::vector<std::thread> load;
+  for (size_t k = 0; k < load_threads; ++k)
+    load.emplace_back([&] {
+      pthread_setname_np(pthread_self(), "load");
+      volatile uint64_t x = 0;
+      while (!load_stop.load(std::memory_order_relaxed))
+        for (int i = 0; i < 4096; ++i) x = x * 6364136223846793005ull + 1;
+    });
   WatchedPool shared(pool);
   std::unique_ptr<Executor> exec(async_threads > 0 ? new Executor(async_threads) : nullptr);
   // Watchdog: a thread blocked in acquire, and nothing moved for deadlock_s.
@@ -528,6 +562,10 @@ int main(int argc, char** argv) {
   }
   finished.store(true);
   watchdog.join();
+  load_stop.store(true);
+  for (auto& t : load) t.join();
+  double cpu_eff = 0;
+  (void)qsmd5_get_cpu_efficiency(&cpu_eff);
   const bool injected = short_read_part || fail_upload_part || check_throws_after != SIZE_MAX;
   for (size_t f = 0; f < files; ++f)
     if (!errors[f].empty()) {
@@ -583,7 +621,8 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < hash_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", hash_runs[i]);
   printf("], \"wall_s_runs\": [");
   for (size_t i = 0; i < wall_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", wall_runs[i]);
-  printf("], \"busy_threads\": {%s}, \"cpu_s_runs\": [", busy_threads().c_str());
+  printf("], \"cpus\": %zu, \"load_threads\": %zu, \"cpu_efficiency\": %.4f", cpus, load_threads, cpu_eff);
+  printf(", \"busy_threads\": {%s}, \"cpu_s_runs\": [", busy_threads().c_str());
   for (size_t i = 0; i < cpu_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", cpu_runs[i]);
   printf("], \"md5\": %s, \"md5_files\": [", md5_list(md5[0]).c_str());
   for (size_t f = 0; f < files; ++f) printf("%s%s", f ? ", " : "", md5_list(md5[f]).c_str());

@@ -112,6 +112,7 @@ def test_auto_mode_without_gpu_falls_back(monkeypatch):
     if qsmd5.device_count() > 0:
         pytest.skip("GPU present")
     monkeypatch.setenv("QSMD5_BACKEND", "auto")
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "0")  # the scalar model: 40 x 256 KiB prices to the GPU
     big = lcg_bytes(12345, 10 << 20)
     many = [(ctypes.addressof(big) + i * (256 << 10), 256 << 10) for i in range(40)]
     before = qsmd5.stats()
@@ -143,6 +144,8 @@ def test_routing_rule(monkeypatch):
     parts and large object batches go to the GPU; the break-even moves with
     QSMD5_CPU_THREADS as the cost model says."""
     monkeypatch.delenv("QSMD5_CPU_THREADS", raising=False)
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "0")  # scalar chains (the lanes: test_lane_priced_*)
+    monkeypatch.setenv("QSMD5_CPU_LOAD_FEEDBACK", "0")  # the idle-host model exactly
     # the rule at the reference rates (the host's own rates: the test below)
     monkeypatch.setenv("QSMD5_CPU_GIBS", "0.7")
     monkeypatch.setenv("QSMD5_GPU_CHAIN_GIBS", "0.119")
@@ -189,9 +192,10 @@ def test_routing_prices_this_hosts_measured_rates(monkeypatch):
     routing decision (qsmd5_get_rates), and the break-even batch moves exactly
     as the cost model predicts when the CPU rate is forced slower or faster
     (QSMD5_CPU_GIBS) or the GPU chain faster (QSMD5_GPU_CHAIN_GIBS)."""
-    for k in ("QSMD5_CPU_GIBS", "QSMD5_GPU_CHAIN_GIBS", "QSMD5_LINK_GIBS", "QSMD5_CPU_THREADS",
-              "QSMD5_ROUTE_LANES"):
+    for k in ("QSMD5_CPU_GIBS", "QSMD5_GPU_CHAIN_GIBS", "QSMD5_LINK_GIBS", "QSMD5_CPU_THREADS"):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "0")  # the scalar model this test restates
+    monkeypatch.setenv("QSMD5_CPU_LOAD_FEEDBACK", "0")
     MiB = 1 << 20
     r = qsmd5.rates()
     assert r["source"] & qsmd5.RATE_CPU_MEASURED and not r["source"] & qsmd5.RATE_CPU_ENV
@@ -241,6 +245,8 @@ def test_split_routing_rule(monkeypatch):
     the GPU hashes the rest (qsmd5_route -> BACKEND_SPLIT).  Equal parts and
     many small objects never split; QSMD5_SPLIT=0 turns it off."""
     monkeypatch.delenv("QSMD5_CPU_THREADS", raising=False)
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "0")
+    monkeypatch.setenv("QSMD5_CPU_LOAD_FEEDBACK", "0")
     monkeypatch.setenv("QSMD5_CPU_GIBS", "0.7")
     monkeypatch.setenv("QSMD5_GPU_CHAIN_GIBS", "0.119")
     monkeypatch.delenv("QSMD5_SPLIT", raising=False)
@@ -263,6 +269,7 @@ def test_split_batch_digests_on_cpu_only_box(monkeypatch):
         pytest.skip("a GPU is visible: routing prices this host's measured rates and the "
                     "batch need not split (the GPU suite covers split batches)")
     monkeypatch.setenv("QSMD5_BACKEND", "auto")
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "0")
     monkeypatch.setenv("QSMD5_CPU_THREADS", "1")  # a small batch that still favours the GPU
     monkeypatch.delenv("QSMD5_SPLIT", raising=False)
     MiB = 1 << 20
@@ -309,7 +316,7 @@ def test_log_callback_carries_backend_without_stderr():
     LogMacros.h) at LogLevel Info, and a GPU that cannot be used at Warn --
     with nothing on stderr, even under QSMD5_LOG=1.  Removing the sink
     restores stderr."""
-    env = dict(os.environ, QSMD5_LOG="1", QSMD5_BACKEND="auto",
+    env = dict(os.environ, QSMD5_LOG="1", QSMD5_BACKEND="auto", QSMD5_ROUTE_LANES="0",
                PYTHONPATH=os.path.join(ROOT, "qsfs-fuse_amd"))
     out = subprocess.run(["python", "-c", LOG_SINK_SCRIPT], env=env, capture_output=True, text=True,
                          timeout=120)
@@ -410,19 +417,21 @@ print("ok", len(chunks))
         assert out.returncode == 0 and out.stdout.startswith("ok"), (mb, out.stdout + out.stderr[-2000:])
 
 
-def test_lane_priced_routing_is_opt_in(monkeypatch, golden):
-    """QSMD5_ROUTE_LANES=1 prices the multi-buffer lanes for host batches:
-    BASELINE config 4's lengths and 64 x 10 MiB then stay on the CPU, 512 x
-    10 MiB still takes the GPU.  Off (the default) the routing is unchanged."""
+def test_lane_priced_routing_is_the_default(monkeypatch, golden):
+    """Round 5: the multi-buffer lanes are priced for host
+    batches by default -- BASELINE config 4's lengths and 64 x 10 MiB stay on
+    the CPU, 512 x 10 MiB at one thread still takes the GPU.  QSMD5_ROUTE_LANES=0
+    restores the scalar model (split / GPU)."""
     if "avx512f" not in open("/proc/cpuinfo").read():
         pytest.skip("host without AVX-512F: the lanes are never priced")
     G, C, S = qsmd5.BACKEND_GPU, qsmd5.BACKEND_CPU, qsmd5.BACKEND_SPLIT
     lens = golden("ragged.json")["lengths"]
     monkeypatch.setenv("QSMD5_CPU_THREADS", "4")
-    monkeypatch.delenv("QSMD5_ROUTE_LANES", raising=False)
+    monkeypatch.setenv("QSMD5_CPU_LOAD_FEEDBACK", "0")
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "0")
     assert qsmd5.route(lens) == S
     assert qsmd5.route([10 * MiB] * 64) == G
-    monkeypatch.setenv("QSMD5_ROUTE_LANES", "1")
+    monkeypatch.delenv("QSMD5_ROUTE_LANES")
     assert qsmd5.route(lens) == C
     assert qsmd5.route([10 * MiB] * 64) == C
     # 512 x 10 MiB is a GPU batch for one CPU thread's lanes on any host; at 4
@@ -434,3 +443,54 @@ def test_lane_priced_routing_is_opt_in(monkeypatch, golden):
     assert qsmd5.route([10 * MiB]) == C  # a lone part: scalar, as before
     monkeypatch.setenv("QSMD5_CPU_MB", "0")  # no lanes, nothing to price
     assert qsmd5.route(lens) == S
+
+
+def test_cpu_load_feedback_moves_batches_to_the_gpu(monkeypatch):
+    """CPU batches timed slower than priced (a host whose
+    cores are busy) lower qsmd5_get_cpu_efficiency, and auto routing then
+    prices the CPU that much slower: a batch on the CPU side of the idle
+    break-even moves to the GPU.  Here the load is simulated by pricing the
+    CPU 8x faster than it runs (QSMD5_CPU_GIBS), so its batches take ~8x their
+    estimate; the value relaxes back to 1 when no CPU batch runs
+    (QSMD5_CPU_EFF_DECAY_S)."""
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "0")
+    monkeypatch.setenv("QSMD5_CPU_MB", "0")  # scalar chains, the rate QSMD5_CPU_GIBS prices
+    monkeypatch.setenv("QSMD5_CPU_THREADS", "1")
+    monkeypatch.setenv("QSMD5_GPU_CHAIN_GIBS", "0.119")
+    monkeypatch.setenv("QSMD5_CPU_LOAD_FEEDBACK", "1")
+    monkeypatch.setenv("QSMD5_CPU_EFF_DECAY_S", "1000")
+    real = qsmd5.rates()["cpu_chain_gibs"]
+    monkeypatch.setenv("QSMD5_CPU_GIBS", "%.4f" % (8 * real))
+    n = next(k for k in range(1, 400) if qsmd5.route([MiB] * (k + 1)) == qsmd5.BACKEND_GPU)
+    assert qsmd5.route([MiB] * n) == qsmd5.BACKEND_CPU  # n: the largest CPU batch of 1 MiB parts
+    data = lcg_bytes(5, 4 * MiB)
+    for _ in range(3):  # three slow CPU batches, priced at >= 2 ms each
+        qsmd5.hash_batch([(ctypes.addressof(data), 4 * MiB)] * 8, flags=CPU)
+    eff = qsmd5.cpu_efficiency()
+    assert eff < 0.5, eff
+    assert qsmd5.route([MiB] * n) == qsmd5.BACKEND_GPU
+    monkeypatch.setenv("QSMD5_CPU_LOAD_FEEDBACK", "0")  # off: the idle-host model again
+    assert qsmd5.cpu_efficiency() == 1.0 and qsmd5.route([MiB] * n) == qsmd5.BACKEND_CPU
+    monkeypatch.setenv("QSMD5_CPU_LOAD_FEEDBACK", "1")
+    monkeypatch.setenv("QSMD5_CPU_EFF_DECAY_S", "0")  # decay "now": the sample has aged out
+    import time
+    time.sleep(0.01)
+    assert qsmd5.cpu_efficiency() > 0.99
+
+
+def test_shutdown_not_starved_by_overlapping_calls(tmp_path):
+    """six threads hash back to back so that some call always holds
+    the runtime's call lock; qsmd5_shutdown must still get through (the gate
+    in CallScope holds new calls back while it is pending) and the threads'
+    later calls must work.  Before the gate it waited until the hashers were
+    stopped (20 s, the program's watchdog)."""
+    exe = str(tmp_path / "shutdown_starvation")
+    subprocess.check_call([
+        "g++", "-std=c++17", "-O2", os.path.join(ROOT, "tests", "cpp", "shutdown_starvation.cpp"),
+        "-I" + os.path.join(ROOT, "include"), "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
+        "-lpthread", "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-o", exe])
+    out = subprocess.run([exe, "6"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    import json
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert not r["starved"] and r["shutdown_s"] < 5.0 and r["calls_after"] > 0

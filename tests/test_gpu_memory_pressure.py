@@ -80,6 +80,7 @@ def test_gpu_out_of_memory_falls_back_to_the_cpu():
     # whole-chunk staging (QSMD5_COLUMN_BYTES=0): the ring then needs >= 512 MiB
     # regions, which cannot fit in the ~256 MiB the hog leaves
     env = dict(os.environ, QSMD5_BACKEND="auto", QSMD5_CPU_THREADS="1", QSMD5_COLUMN_BYTES="0",
+               QSMD5_ROUTE_LANES="0",  # the scalar model: the batch prices to the GPU
                PYTHONPATH=os.pathsep.join([os.path.join(ROOT, "qsfs-fuse_amd"), os.path.join(ROOT, "tests")]))
     env.pop("QSMD5_INJECT_GPU_FAULT", None)
     out = subprocess.run([sys.executable, "-c", SCRIPT], env=env, capture_output=True, text=True,

@@ -51,11 +51,18 @@ def test_whole_file_wave_on_the_gpu(gold, pinned, slab):
 def test_default_pool_routes_waves_by_size(gold):
     """auto: qsfs's default pool (5 x 10 MiB buffers, 50 MiB heap) gives waves
     below the GPU break-even, hashed on the CPU; a 64-buffer pool's waves go to
-    the gfx950 kernels.  Same golden digests either way."""
+    the gfx950 kernels under the scalar model (QSMD5_ROUTE_LANES=0) and to the
+    CPU's AVX-512 lanes, ~3x faster on this host, under the default lane
+    pricing.  Same golden digests every way."""
     small = run(["--aligned", "--size=%d" % (64 * 10 * MiB), "--pool=5", "--no-pipeline"], "auto")
     assert small["waves"] == 13 and small["cpu_waves"] == 13 and small["gpu_waves"] == 0
-    big = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=64", "--no-pipeline"], "auto")
+    big = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=64", "--no-pipeline"], "auto",
+              extra_env={"QSMD5_ROUTE_LANES": "0"})
     assert big["waves"] == 2 and big["gpu_waves"] == 2
+    lanes = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=64", "--no-pipeline"], "auto")
+    if "avx512f" in open("/proc/cpuinfo").read():
+        assert lanes["cpu_waves"] == 2, lanes
+    assert lanes["md5"] == gold[:128]
     assert small["md5"] == gold[:64] and big["md5"] == gold[:128]
     print("64 parts, pool 5 (CPU waves): hash %.3f s; 128 parts, pool 64 (GPU waves): hash %.3f s"
           % (small["hash_s"], big["hash_s"]))

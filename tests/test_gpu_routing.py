@@ -33,6 +33,10 @@ def auto(monkeypatch):
         pytest.skip("no GPU")
     monkeypatch.setenv("QSMD5_BACKEND", "auto")
     monkeypatch.delenv("QSMD5_INJECT_GPU_FAULT", raising=False)
+    # the scalar idle-host model these tests restate (lanes and load feedback:
+    # test_lane_priced_* below, tests/test_cpu_backend.py)
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "0")
+    monkeypatch.setenv("QSMD5_CPU_LOAD_FEEDBACK", "0")
     assert qsmd5.lib().qsmd5_init(0) == 0
 
 
@@ -248,10 +252,10 @@ def test_split_config4_device_resident(auto, golden):
 
 
 def test_lane_priced_routing_keeps_host_batch_on_cpu(auto, monkeypatch):
-    """QSMD5_ROUTE_LANES=1 on the box's host CPU: a ragged host batch (62
-    chunks, 1-16 MiB) stays on the CPU's multi-buffer lanes instead of
-    splitting, and every digest equals the oracle's; without the knob it
-    splits as before."""
+    """Lanes priced (the default since round 5) on the box's host CPU: a
+    ragged host batch (62 chunks, 1-16 MiB) stays on the CPU's multi-buffer
+    lanes instead of splitting, and every digest equals the oracle's; with
+    QSMD5_ROUTE_LANES=0 it splits as before."""
     if "avx512f" not in open("/proc/cpuinfo").read():
         pytest.skip("host without AVX-512F: the lanes are never priced")
     monkeypatch.setenv("QSMD5_CPU_THREADS", "1")  # one thread: the scalar model splits
@@ -263,7 +267,7 @@ def test_lane_priced_routing_keeps_host_batch_on_cpu(auto, monkeypatch):
     assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
     s1 = qsmd5.stats()
     assert s1["gpu_batches"] == s0["gpu_batches"] and s1["cpu_chunks"] - s0["cpu_chunks"] == len(lens)
-    monkeypatch.delenv("QSMD5_ROUTE_LANES")
+    monkeypatch.setenv("QSMD5_ROUTE_LANES", "0")
     assert qsmd5.route(lens) == qsmd5.BACKEND_SPLIT
 
 

@@ -145,6 +145,7 @@ def _run(variant, devices, threads=6, rounds=12, max_len=3 << 20, extra=(), expe
         env["QSMD5_CPU_THREADS"] = str(cpu_threads)
     if backend == "auto":
         env["QSMD5_LOG"] = "1"  # the routing decisions, checked below
+        env["QSMD5_ROUTE_LANES"] = "0"  # the scalar model, under which ragged batches split
     env.pop("QSMD5_DEVICES", None)
     if devices:
         env["QSMD5_DEVICES"] = devices
