@@ -19,6 +19,8 @@ Further lines, on request:
   pool   512 pool buffers passed in pool order and shuffled
   tiny   device-resident 1 M x 1 KiB, 1 M x 4 KiB, 512 K x 16 KiB
   satpad saturation at exact power-of-two strides vs padded
+  satsweep / sat64 / sat256  the coalesced kernel at 131072 x {16..256} KiB, or one
+     of the two sat lines alone (scripts/r05_sat_attrib.sh: PMC passes per size)
 
 Every digest is checked against the reference-produced golden fixtures where
 they exist.  One JSON object per config on stdout.
@@ -431,6 +433,14 @@ def main():
             for L, n in ((1024, 1 << 20), (4096, 1 << 20), (16384, 1 << 19)):
                 saturation(args.reps, L=L, pad=0, n=n)
                 torch.cuda.empty_cache()
+        elif c == "satsweep":  # round 5: the coalesced kernel's rate against chunk length
+            for kib in (16, 32, 64, 128, 256):
+                saturation(args.reps, L=kib * 1024)
+                torch.cuda.empty_cache()
+        elif c == "sat64":
+            saturation(args.reps)
+        elif c == "sat256":
+            saturation(args.reps, L=256 * 1024)
         elif c == "pool":
             pool(args.reps)
         elif c == "sat":
