@@ -461,12 +461,22 @@ static bool lanes_priced(const qsmd5_chunk* chunks, size_t n, int flags) {
 }
 
 // The lanes' idle-host model: the longest chain in one lane, or all bytes over
-// T threads' lanes together.
-static double lanes_model_ms(uint64_t longest, uint64_t total) {
-  const double lt = cpu_rates().lane_thread;  // a lane's chain: 1/(16 x groups) of it
-  const double lanes_per_thread = 16.0 * cpu_rates().mb_groups;
-  return 1e3 * std::max((double)longest / (lt / lanes_per_thread),
-                        (double)total / ((double)cpu_threads() * lt)) / kGiB;
+// T threads' lanes together -- with the lane count cpu_batch will run: two
+// groups (32 lanes, lane32) only where this core timed them faster AND the
+// batch fills 32 lanes on every thread AND they come out ahead, else one
+// (16 lanes, lane16).  Pricing a half-filled batch at 32 lanes' chain rate
+// would double its estimate.
+static double lanes_est_ms(double rate, double lanes, uint64_t longest, uint64_t total, double T) {
+  return 1e3 * std::max((double)longest / (rate / lanes), (double)total / (T * rate)) / kGiB;
+}
+static double lanes_model_ms(uint64_t longest, uint64_t total, size_t n) {
+  const CpuRates& c = cpu_rates();
+  const double T = (double)std::min<size_t>(cpu_threads(), std::max<size_t>(n, 1));
+  const double r16 = c.lane16 > 0 ? c.lane16 : c.lane_thread;
+  double ms = lanes_est_ms(r16, 16.0, longest, total, T);
+  if (c.mb_groups == 2 && c.lane32 > 0 && (double)n >= 32.0 * T)
+    ms = std::min(ms, lanes_est_ms(c.lane32, 32.0, longest, total, T));
+  return ms;
 }
 
 // True when the CPU is expected to finish this batch first (see above).  The
@@ -484,7 +494,7 @@ bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags) {
   const bool lanes = lanes_priced(chunks, n, flags);  // only for all-host batches
   auto cpu_ms_of = [&](uint64_t d2h) {
     if (!lanes) return cpu_est_ms(longest, total, d2h);
-    return lanes_model_ms(longest, total) / cpu_efficiency();
+    return lanes_model_ms(longest, total, n) / cpu_efficiency();
   };
   if (!(cpu_ms_of(0) < gpu_est_ms(longest, total))) return false;
   if (lanes || (flags & QSMD5_FLAG_HOST) || qsmd5_device_count() <= 0) return true;
@@ -518,7 +528,7 @@ double cpu_priced_ms(const qsmd5_chunk* chunks, size_t n, int flags) {
   }
   const bool mb = env_u64("QSMD5_CPU_MB", 1) && qsmd5::cpu::mb16_available() &&
                   cpu_rates().lane_thread > 0 && n >= 2 * std::min<size_t>(cpu_threads(), n);
-  return mb ? lanes_model_ms(longest, total) : cpu_model_ms(longest, total);
+  return mb ? lanes_model_ms(longest, total, n) : cpu_model_ms(longest, total);
 }
 
 // Ragged batches (qsfs -b sweeps, a file's parts plus small files): the GPU's

@@ -445,6 +445,10 @@ int main(int argc, char** argv) {
       while (!load_stop.load(std::memory_order_relaxed))
         for (int i = 0; i < 4096; ++i) x = x * 6364136223846793005ull + 1;
     });
+  // The scheduler gives threads it has just started less than their share
+  // for a while (the first pass of a --load run hashed as fast as an idle
+  // one, later passes half as fast): let the load settle before timing.
+  if (load_threads) std::this_thread::sleep_for(std::chrono::seconds(1));
   WatchedPool shared(pool);
   std::unique_ptr<Executor> exec(async_threads > 0 ? new Executor(async_threads) : nullptr);
   // Watchdog: a thread blocked in acquire, and nothing moved for deadlock_s.

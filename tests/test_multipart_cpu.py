@@ -252,3 +252,22 @@ def test_staged_cancel_stops_between_parts():
              "--cancel-after=6"], "cpu")
     assert r["stopped"] == 1 and r["uploaded"] == 6 and r["stats_uploaded"] == 6
     assert r["pool_free_after"] == 5
+
+
+def test_busy_cores_lower_the_cpu_efficiency():
+    """VERDICT r04 item 3's load, as scripts/r05_route_sweep.sh sets it up: the
+    harness held to 2 cores (--cpus=2) with 2 spinning threads of other work on
+    them (--load=2).  The CPU backend's waves then take longer than priced, and
+    qsmd5_get_cpu_efficiency (the factor auto routing divides CPU estimates by)
+    reads well below 1; on the same cores without the load it stays near 1.
+    Every digest stays golden."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    base = ["--aligned", "--size=%d" % (16 * 10 * MiB), "--pool=8", "--no-pipeline", "--repeat=2",
+            "--cpus=2"]
+    env = {"QSMD5_CPU_THREADS": "2", "QSMD5_CPU_EFF_DECAY_S": "1000"}
+    idle = run(base + ["--load=0"], "cpu", extra_env=env)
+    busy = run(base + ["--load=2"], "cpu", extra_env=env)
+    assert idle["md5"] == gold[:16] and busy["md5"] == gold[:16]
+    assert busy["cpus"] == 2 and busy["load_threads"] == 2
+    assert busy["cpu_efficiency"] < 0.75, busy["cpu_efficiency"]
+    assert busy["cpu_efficiency"] < idle["cpu_efficiency"] - 0.2, (idle["cpu_efficiency"], busy["cpu_efficiency"])
