@@ -403,6 +403,12 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
 struct StagedOptions {
   uint64_t staging_bytes = 0;  // qsmd5_hash_read's budget (0: QSMD5_READ_STAGING_BYTES, 256 MiB)
   size_t wave_parts = 0;       // parts per pre-hash call (0: every part of the file at once)
+  // Ramp (with pipeline and wave_parts): the first wave has this many parts
+  // and each next one twice the last, up to wave_parts (0: every wave
+  // wave_parts).  The first upload then waits only for a small wave (the
+  // CPU's, ~ms) instead of a GPU wave's chain time (~85 ms per 10 MiB part),
+  // and each larger wave is pre-hashed while the smaller one before it uploads.
+  size_t first_wave_parts = 0;
   bool pipeline = true;        // pre-hash the next wave on a helper thread while this one uploads
   bool upload_releases = false;  // as PrehashOptions::upload_releases
   int flags = 0;               // qsmd5_hash_read flags (QSMD5_FLAG_GPU_ONLY / _CPU_ONLY)
@@ -499,8 +505,13 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
   const auto t_start = clock::now();
   if (parts.empty()) return st;
   const size_t per = opt.wave_parts ? opt.wave_parts : parts.size();
-  auto prep = [&](size_t first) {
-    return detail::prehash_wave(parts, first, std::min(per, parts.size() - first), read_range, opt);
+  // the size of the wave after one of `prev` parts (0: the first wave)
+  auto wave_size = [&](size_t prev) {
+    if (!opt.first_wave_parts || !opt.wave_parts || !opt.pipeline) return per;
+    return prev ? std::min(per, 2 * prev) : std::min(per, opt.first_wave_parts);
+  };
+  auto prep = [&](size_t first, size_t count) {
+    return detail::prehash_wave(parts, first, std::min(count, parts.size() - first), read_range, opt);
   };
   std::future<detail::StagedWave> ahead;
   auto drain_ahead = [&]() noexcept {
@@ -512,7 +523,7 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
   };
   auto stop_requested = [&] { return opt.should_continue && !opt.should_continue(); };
   const auto tw = clock::now();
-  detail::StagedWave cur = prep(0);
+  detail::StagedWave cur = prep(0, wave_size(0));
   st.wait_s += secs(tw, clock::now());
   for (;;) {
     if (cur.cancelled) {
@@ -531,7 +542,7 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
     }
     if (opt.pipeline && next < parts.size()) {
       try {
-        ahead = std::async(std::launch::async, prep, next);
+        ahead = std::async(std::launch::async, prep, next, wave_size(n));
       } catch (...) {
         // no thread or no memory for one: the next wave is pre-hashed here, after this one
       }
@@ -572,7 +583,7 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
     }
     if (next >= parts.size()) break;
     const auto t1 = clock::now();
-    cur = ahead.valid() ? ahead.get() : prep(next);
+    cur = ahead.valid() ? ahead.get() : prep(next, wave_size(n));
     st.wait_s += secs(t1, clock::now());
   }
   st.wall_s = secs(t_start, clock::now());

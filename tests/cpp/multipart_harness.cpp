@@ -316,7 +316,7 @@ int main(int argc, char** argv) {
   size_t pool_n = 5, files = 1, naive_wave = 0, max_wave = 0;
   bool aligned = false, pinned = false, slab = false, reg = false, pipeline = true, staged = false;
   uint64_t staging = 0;
-  size_t wave_parts = 0;
+  size_t wave_parts = 0, first_wave = 0;
   size_t cpus = 0, load_threads = 0;  // --cpus: the process's cores; --load: spinning threads on them
   uint32_t seed = 12345;
   uint64_t buf = 10ull << 20;
@@ -345,6 +345,7 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--check-throws-after=")) check_throws_after = strtoull(v, nullptr, 0);
     else if (const char* v = val("--staging=")) staging = strtoull(v, nullptr, 0);
     else if (const char* v = val("--wave-parts=")) wave_parts = strtoull(v, nullptr, 0);
+    else if (const char* v = val("--first-wave=")) first_wave = strtoull(v, nullptr, 0);
     else if (const char* v = val("--cpus=")) cpus = strtoull(v, nullptr, 0);
     else if (const char* v = val("--load=")) load_threads = strtoull(v, nullptr, 0);
     else if (a == "--staged") staged = true;
@@ -538,6 +539,7 @@ int main(int argc, char** argv) {
               qsmd5::StagedOptions so;
               so.staging_bytes = staging;
               so.wave_parts = wave_parts;
+              so.first_wave_parts = first_wave;
               so.pipeline = pipeline;
               so.upload_releases = opt.upload_releases;
               so.should_continue = opt.should_continue;
@@ -625,7 +627,8 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < hash_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", hash_runs[i]);
   printf("], \"wall_s_runs\": [");
   for (size_t i = 0; i < wall_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", wall_runs[i]);
-  printf("], \"cpus\": %zu, \"load_threads\": %zu, \"cpu_efficiency\": %.4f", cpus, load_threads, cpu_eff);
+  printf("], \"cpus\": %zu, \"load_threads\": %zu, \"cpu_efficiency\": %.4f, \"wave_parts\": %zu, \"first_wave\": %zu",
+         cpus, load_threads, cpu_eff, wave_parts, first_wave);
   printf(", \"busy_threads\": {%s}, \"cpu_s_runs\": [", busy_threads().c_str());
   for (size_t i = 0; i < cpu_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", cpu_runs[i]);
   printf("], \"md5\": %s, \"md5_files\": [", md5_list(md5[0]).c_str());

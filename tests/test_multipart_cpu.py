@@ -209,6 +209,20 @@ def test_staged_prehash_matches_golden(extra):
     assert r["waves"] == want_waves and r["widest_wave"] == (5 if want_waves == 5 else 24)
 
 
+@pytest.mark.parametrize("extra,waves", [(["--wave-parts=8", "--first-wave=2"], [2, 4, 8, 8, 2]),
+                                         (["--wave-parts=8", "--first-wave=2", "--no-pipeline"], [8, 8, 8]),
+                                         (["--wave-parts=64", "--first-wave=3"], [3, 6, 12, 3])])
+def test_staged_wave_ramp(extra, waves):
+    """StagedOptions::first_wave_parts: with the pipeline, the first wave is
+    small and each next one doubles up to wave_parts (the first upload waits
+    for a CPU-sized wave, every larger wave is pre-hashed while the smaller one
+    uploads); without the pipeline the ramp is off.  Same golden digests."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    r = run(["--aligned", "--size=%d" % (24 * 10 * MiB), "--pool=5", "--staged", "--upload-ms=1"] + extra, "cpu")
+    assert r["md5"] == gold[:24] and r["uploaded"] == 24 and r["pool_free_after"] == 5
+    assert r["waves"] == len(waves) and r["widest_wave"] == max(waves), (r["waves"], r["widest_wave"])
+
+
 def test_staged_ragged_file_matches_oracle():
     for size, seed in ((25 * MiB + 3, 41), (100 * MiB + 12345, 42)):
         r = run(["--size=%d" % size, "--seed=%d" % seed, "--pool=2", "--staged",
