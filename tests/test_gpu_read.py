@@ -188,3 +188,20 @@ def test_staged_prehash_default_pool(parts):
     wall = min(r["wall_s_runs"])
     print("%d x 10 MiB, -n 5, staged: %.3f s end to end (%.2f GiB/s), pre-hash %.3f s"
           % (parts, wall, gib / wall, r["hash_s"]))
+
+
+def test_staged_ramp_hides_gpu_waves_behind_uploads():
+    """StagedOptions::first_wave_parts on the box: 128 parts at -n 5, waves
+    4, 8, 16, 32, 64, 4 pipelined against 5 ms uploads.  The small first wave
+    is routed to the CPU, the 64-part wave to the GPU, every digest is golden,
+    and the uploader waits only for the first wave: the GPU's chain time hides
+    behind the uploads of the waves before it."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    r = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=5", "--pinned", "--staged",
+             "--wave-parts=64", "--first-wave=4", "--upload-ms=5"], "auto", timeout=600)
+    assert r["md5"] == gold[:128] and r["pool_free_after"] == 5 and r["uploaded"] == 128
+    assert r["waves"] == 6 and r["widest_wave"] == 64
+    assert r["gpu_waves"] >= 1 and r["cpu_waves"] >= 1, r
+    assert r["wait_s"] < 0.5 * r["hash_s"], (r["wait_s"], r["hash_s"])
+    print("ramp: %d waves (gpu %d, cpu %d), hash %.3f s, uploader waited %.3f s, wall %.3f s"
+          % (r["waves"], r["gpu_waves"], r["cpu_waves"], r["hash_s"], r["wait_s"], r["wall_s_runs"][-1]))
