@@ -174,6 +174,23 @@ struct EventSet {
   }
 };
 
+// One pull-driven batch in flight (qsmd5_hash_read, qsmd5_rt_read.cpp): its
+// stream, events and buffers.  A job runs for as long as the caller's reads
+// take, so it must not hold Dev::mu (every other batch on this GPU) meanwhile;
+// and jobs of different files (qsfs flushes files from several FUSE threads at
+// once) each read on their own thread, so a GPU keeps up to
+// QSMD5_READ_SLOTS (default 2, at most kMaxReadSlots) of them running side
+// by side.  The stream and events are made on first use, the buffers grow
+// with the jobs (HostPinned / DevBuf reserve).
+constexpr int kMaxReadSlots = 8;
+struct ReadSlot {
+  hipStream_t stream = nullptr;
+  hipEvent_t copied[2] = {};  // the last H2D copy out of host region k
+  hipEvent_t done = nullptr;
+  HostPinned h_read, h_meta;  // two staging regions; descriptors + orders, then digests
+  DevBuf d_read, d_meta, d_state, d_dig;
+};
+
 // One bound GPU: its streams, scratch and staging ring.  Batches on one Dev are
 // serialised by its mutex; different Devs run concurrently (multi-GPU shards).
 struct Dev {
@@ -192,15 +209,13 @@ struct Dev {
   uint64_t staging_cap = kDefaultStaging;
   double last_wall_ms = 0, last_kernel_ms = 0;
   std::atomic<uint32_t> chain_samples{0};  // batches that qualified as a chain-rate sample
-  // Pull-driven batches (qsmd5_hash_read, qsmd5_rt_read.cpp) have their own
-  // lock, stream and buffers: a job runs for as long as the caller's reads
-  // take, and must not hold `mu` (every other batch on this GPU) meanwhile.
+  // Pull-driven batches: slots taken under read_mu, a job waits on read_cv
+  // while all nread_slots are busy (qsmd5_rt_read.cpp).
   std::mutex read_mu;
-  hipStream_t read_stream = nullptr;
-  hipEvent_t read_copied[2] = {};  // the last H2D copy out of host region k
-  hipEvent_t read_done = nullptr;
-  HostPinned h_read, h_read_meta;  // two staging regions; descriptors + orders, then digests
-  DevBuf d_read, d_read_meta, d_read_state, d_read_dig;
+  std::condition_variable read_cv;
+  uint32_t read_busy = 0;  // bit k: slot k has a job
+  int nread_slots = 2;
+  ReadSlot read_slot[kMaxReadSlots];
 };
 
 struct Runtime {

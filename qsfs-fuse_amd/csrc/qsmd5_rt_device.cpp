@@ -132,11 +132,7 @@ static int init_dev(Dev& d, int device) {
       (e = hipEventCreateWithFlags(&d.ev_done, hipEventBlockingSync | hipEventDisableTiming)) !=
           hipSuccess)
     return hip_fail(e, "hipEventCreate");
-  if ((e = hipStreamCreateWithFlags(&d.read_stream, hipStreamNonBlocking)) != hipSuccess)
-    return hip_fail(e, "hipStreamCreate");
-  for (hipEvent_t* ev : {&d.read_copied[0], &d.read_copied[1], &d.read_done})
-    if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess)
-      return hip_fail(e, "hipEventCreate");
+  d.nread_slots = (int)std::min<uint64_t>(kMaxReadSlots, std::max<uint64_t>(1, env_u64("QSMD5_READ_SLOTS", 2)));
   if ((e = qsmd5::warm_up(d.compute[0])) != hipSuccess ||
       (e = hipStreamSynchronize(d.compute[0])) != hipSuccess)
     return hip_fail(e, "qsmd5: kernel warm-up (is this a gfx950 GPU?)");
@@ -168,30 +164,42 @@ int release_dev(Dev& d) {
       chk(hipStreamDestroy(s));
       s = nullptr;
     }
-  if (d.read_stream) {
-    chk(hipStreamSynchronize(d.read_stream));
-    chk(hipStreamDestroy(d.read_stream));
-    d.read_stream = nullptr;
+  for (ReadSlot& rs : d.read_slot) {
+    if (rs.stream) {
+      chk(hipStreamSynchronize(rs.stream));
+      chk(hipStreamDestroy(rs.stream));
+      rs.stream = nullptr;
+    }
+    for (hipEvent_t* e : {&rs.copied[0], &rs.copied[1], &rs.done})
+      if (*e) {
+        chk(hipEventDestroy(*e));
+        *e = nullptr;
+      }
   }
-  for (hipEvent_t* e : {&d.ev_meta, &d.ev_first, &d.ev_last, &d.ev_done, &d.read_copied[0],
-                        &d.read_copied[1], &d.read_done})
+  for (hipEvent_t* e : {&d.ev_meta, &d.ev_first, &d.ev_last, &d.ev_done})
     if (*e) {
       chk(hipEventDestroy(*e));
       *e = nullptr;
     }
-  for (DevBuf* b : {&d.d_meta, &d.d_dig, &d.d_staging, &d.d_state, &d.d_read, &d.d_read_meta,
-                    &d.d_read_state, &d.d_read_dig})
+  std::vector<DevBuf*> dbufs = {&d.d_meta, &d.d_dig, &d.d_staging, &d.d_state};
+  std::vector<HostPinned*> hbufs = {&d.h_meta, &d.h_dig};
+  for (ReadSlot& rs : d.read_slot) {
+    for (DevBuf* b : {&rs.d_read, &rs.d_meta, &rs.d_state, &rs.d_dig}) dbufs.push_back(b);
+    for (HostPinned* b : {&rs.h_read, &rs.h_meta}) hbufs.push_back(b);
+  }
+  for (DevBuf* b : dbufs)
     if (b->p) {
       chk(hipFree(b->p));
       b->p = nullptr;
       b->cap = 0;
     }
-  for (HostPinned* b : {&d.h_meta, &d.h_dig, &d.h_read, &d.h_read_meta})
+  for (HostPinned* b : hbufs)
     if (b->p) {
       chk(hipHostFree(b->p));
       b->p = nullptr;
       b->cap = 0;
     }
+  d.read_busy = 0;
   d.device = -1;
   return bad;
 }

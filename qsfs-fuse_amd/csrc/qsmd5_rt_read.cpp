@@ -12,7 +12,9 @@
 // loaded file), and every part of the file is its own chain, parked between
 // windows: the batch is as wide as the file, the staging stays bounded.
 //
-// Schedule on the GPU (one stream, qsmd5_plan.h plan_read): step s = (group,
+// Schedule on the GPU (the job's read slot: its own stream and buffers, up to
+// QSMD5_READ_SLOTS jobs side by side, qsmd5_rt.h ReadSlot; qsmd5_plan.h
+// plan_read): step s = (group,
 // column).  The calling thread fills host region s % 2 through the caller's
 // reads, then enqueues its H2D copy into the one device region and the column
 // kernel that hashes it.  Stream order keeps the device region safe (copy s+1
@@ -70,23 +72,69 @@ int poll_event(hipEvent_t ev, const char* what) {
   }
 }
 
+// A read slot of `r` for this job (qsmd5_rt.h ReadSlot): the first free one,
+// or wait until a job returns one.  Its stream and events are made on first use.
+struct SlotLease {
+  Dev& r;
+  int k = -1;
+  explicit SlotLease(Dev& dev) : r(dev) {
+    std::unique_lock<std::mutex> lk(r.read_mu);
+    r.read_cv.wait(lk, [&] {
+      for (int i = 0; i < r.nread_slots; ++i)
+        if (!(r.read_busy & (1u << i))) {
+          k = i;
+          return true;
+        }
+      return false;
+    });
+    r.read_busy |= 1u << k;
+  }
+  ~SlotLease() {
+    {
+      std::lock_guard<std::mutex> lk(r.read_mu);
+      r.read_busy &= ~(1u << k);
+    }
+    r.read_cv.notify_one();
+  }
+  SlotLease(const SlotLease&) = delete;
+  SlotLease& operator=(const SlotLease&) = delete;
+  int ready(ReadSlot** out) {
+    ReadSlot& rs = r.read_slot[k];
+    hipError_t e;
+    if (!rs.stream && (e = hipStreamCreateWithFlags(&rs.stream, hipStreamNonBlocking)) != hipSuccess) {
+      rs.stream = nullptr;
+      return hip_fail(e, "hipStreamCreate");
+    }
+    for (hipEvent_t* ev : {&rs.copied[0], &rs.copied[1], &rs.done})
+      if (!*ev && (e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) {
+        *ev = nullptr;
+        return hip_fail(e, "hipEventCreate");
+      }
+    *out = &rs;
+    return 0;
+  }
+};
+
 int gpu_read(Dev& r, ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
-  std::lock_guard<std::mutex> lk(r.read_mu);
+  SlotLease lease(r);
+  ReadSlot* slot = nullptr;
+  if (int rc = lease.ready(&slot)) return rc;
+  ReadSlot& rs = *slot;
   const size_t n = J.len.size();
   const ReadPlan P = plan_read(J.sorted, staging);
   uint64_t region = 0;
   for (const ReadGroup& g : P.groups) region = std::max<uint64_t>(region, g.count * g.stride);
   const size_t desc_span = (n * sizeof(qsmd5_chunk) + 255) & ~size_t(255);
   const size_t meta_bytes = desc_span + n * sizeof(uint32_t);
-  if (int rc = r.h_read.reserve(2 * region)) return rc;
-  if (int rc = r.d_read.reserve(region)) return rc;
-  if (int rc = r.h_read_meta.reserve(std::max<size_t>(meta_bytes, 16 * n))) return rc;
-  if (int rc = r.d_read_meta.reserve(meta_bytes)) return rc;
-  if (int rc = r.d_read_state.reserve(16 * n)) return rc;
-  if (int rc = r.d_read_dig.reserve(16 * n)) return rc;
-  uint8_t* hm = static_cast<uint8_t*>(r.h_read_meta.p);
-  uint8_t* dm = static_cast<uint8_t*>(r.d_read_meta.p);
-  uint8_t* dstage = static_cast<uint8_t*>(r.d_read.p);
+  if (int rc = rs.h_read.reserve(2 * region)) return rc;
+  if (int rc = rs.d_read.reserve(region)) return rc;
+  if (int rc = rs.h_meta.reserve(std::max<size_t>(meta_bytes, 16 * n))) return rc;
+  if (int rc = rs.d_meta.reserve(meta_bytes)) return rc;
+  if (int rc = rs.d_state.reserve(16 * n)) return rc;
+  if (int rc = rs.d_dig.reserve(16 * n)) return rc;
+  uint8_t* hm = static_cast<uint8_t*>(rs.h_meta.p);
+  uint8_t* dm = static_cast<uint8_t*>(rs.d_meta.p);
+  uint8_t* dstage = static_cast<uint8_t*>(rs.d_read.p);
   // Lane k of group g reads its window from the device region's row k; the
   // descriptor carries the chunk's whole length (the column kernel's segment
   // form: it finishes the chain in the column that holds the chunk's end).
@@ -98,7 +146,7 @@ int gpu_read(Dev& r, ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
       hd[g.first + k] = qsmd5_chunk{dstage + k * g.stride, J.len[c]};
       ho[g.first + k] = c;
     }
-  const hipStream_t s = r.read_stream;
+  const hipStream_t s = rs.stream;
   // After a failure, let everything enqueued finish before returning: a copy
   // may still be reading a host region the next call refills.
   auto drain = [&](int rc) {
@@ -110,22 +158,22 @@ int gpu_read(Dev& r, ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
     return drain(rc);
   const qsmd5_chunk* d_desc = reinterpret_cast<const qsmd5_chunk*>(dm);
   const uint32_t* d_ord = reinterpret_cast<const uint32_t*>(dm + desc_span);
-  uint32_t* d_dig = static_cast<uint32_t*>(r.d_read_dig.p);
-  uint32_t* d_state = static_cast<uint32_t*>(r.d_read_state.p);
-  uint8_t* hstage = static_cast<uint8_t*>(r.h_read.p);
+  uint32_t* d_dig = static_cast<uint32_t*>(rs.d_dig.p);
+  uint32_t* d_state = static_cast<uint32_t*>(rs.d_state.p);
+  uint8_t* hstage = static_cast<uint8_t*>(rs.h_read.p);
   size_t step = 0;
   for (const ReadGroup& g : P.groups)
     for (uint32_t j = 0; j < g.ncols; ++j, ++step) {
       const int reg = (int)(step & 1);
       uint8_t* host = hstage + reg * region;
       if (step >= 2)  // the copy that last read this region (step - 2) has finished
-        if (int rc = poll_event(r.read_copied[reg], "qsmd5_hash_read: staging copy")) return drain(rc);
+        if (int rc = poll_event(rs.copied[reg], "qsmd5_hash_read: staging copy")) return drain(rc);
       const size_t act = ReadPlan::active(J.sorted, g, j);
       if (int rc = fill_window(J, g, j, act, host)) return drain(rc);
       if (int rc = hip(hipMemcpyAsync(dstage, host, act * g.stride, hipMemcpyHostToDevice, s),
                        "hipMemcpyAsync H2D"))
         return drain(rc);
-      if (int rc = hip(hipEventRecord(r.read_copied[reg], s), "hipEventRecord")) return drain(rc);
+      if (int rc = hip(hipEventRecord(rs.copied[reg], s), "hipEventRecord")) return drain(rc);
       if (int rc = hip(qsmd5::launch_column(d_desc + g.first, d_ord + g.first, (uint32_t)act, d_dig,
                                             (uint64_t)j * g.W, g.W, d_state, s),
                        "qsmd5 column kernel launch"))
@@ -134,8 +182,8 @@ int gpu_read(Dev& r, ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
   // the metadata's H2D ran first on this stream: its host block is free for the digests
   if (int rc = hip(hipMemcpyAsync(hm, d_dig, 16 * n, hipMemcpyDeviceToHost, s), "hipMemcpyAsync D2H"))
     return drain(rc);
-  if (int rc = hip(hipEventRecord(r.read_done, s), "hipEventRecord")) return drain(rc);
-  if (int rc = poll_event(r.read_done, "qsmd5_hash_read: waiting for the batch")) return drain(rc);
+  if (int rc = hip(hipEventRecord(rs.done, s), "hipEventRecord")) return drain(rc);
+  if (int rc = poll_event(rs.done, "qsmd5_hash_read: waiting for the batch")) return drain(rc);
   memcpy(digests, hm, 16 * n);
   return 0;
 }

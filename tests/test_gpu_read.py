@@ -205,3 +205,19 @@ def test_staged_ramp_hides_gpu_waves_behind_uploads():
     assert r["wait_s"] < 0.5 * r["hash_s"], (r["wait_s"], r["hash_s"])
     print("ramp: %d waves (gpu %d, cpu %d), hash %.3f s, uploader waited %.3f s, wall %.3f s"
           % (r["waves"], r["gpu_waves"], r["cpu_waves"], r["hash_s"], r["wait_s"], r["wall_s_runs"][-1]))
+
+
+@pytest.mark.parametrize("slots", ["1", "2", "4"])
+def test_concurrent_files_read_slots(slots):
+    """Four files flushed at once (four threads, one blocking 5-buffer pool),
+    each pre-hashed as one pull-driven GPU batch: with QSMD5_READ_SLOTS = 1
+    the jobs queue for the one slot; with 2 and 4 they run side by side, each
+    on its own stream and staging.  Every part of every file is golden either
+    way and every pool buffer comes back."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    r = run(["--aligned", "--size=%d" % (64 * 10 * MiB), "--pool=5", "--pinned", "--staged", "--files=4",
+             "--repeat=2"], "gpu", timeout=600, extra_env={"QSMD5_READ_SLOTS": slots})
+    assert r["files"] == 4 and all(m == gold[:64] for m in r["md5_files"])
+    assert r["gpu_waves"] == 4 and r["pool_free_after"] == 5
+    print("QSMD5_READ_SLOTS=%s: 4 files x 64 parts in %.3f s (%.2f GiB/s)"
+          % (slots, r["wall_s_runs"][-1], 4 * 640 / 1024.0 / r["wall_s_runs"][-1]))
