@@ -607,6 +607,104 @@ static double run_issue(ukern k, int instr_per_iter, int iters, int threads) {
   return (double)cyc / ((double)iters * instr_per_iter);
 }
 
+// ---- 1b. Stamped coalesced kernel (round 5) ---------------
+// Diagnostic build of qsmd5_batch_coal_kernel: each wave stamps its start and
+// end in shader cycles (s_memtime) and in the 100 MHz constant clock
+// (s_memrealtime) into a buffer of its own that no other code reads; no
+// output is computed from them.  Splits a dispatch's time into the clock the
+// waves ran at and the spread of wave start / end times (ramp and tail).
+__global__ __launch_bounds__(64) void k_coal_stamped(const ChunkDesc* __restrict__ chunks, uint32_t n,
+                                                     uint32_t* __restrict__ digests, uint64_t* stamps) {
+  const uint64_t c0 = __builtin_amdgcn_s_memtime();
+  const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
+  batch_coal_body<2, 2>(chunks, nullptr, n, digests);
+  const uint64_t c1 = __builtin_amdgcn_s_memtime();
+  const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    uint64_t* q = stamps + 4ull * blockIdx.x;
+    q[0] = c0;
+    q[1] = r0;
+    q[2] = c1;
+    q[3] = r1;
+  }
+}
+
+static double pctl(std::vector<double> v, double q) {
+  std::sort(v.begin(), v.end());
+  return v[(size_t)std::min<double>(v.size() - 1, q * (v.size() - 1) + 0.5)];
+}
+
+// One line per launch of n x L (stride L + pad): event ms, the waves' median
+// clock, start and end spread, and the share of (first start .. last end)
+// an average wave is alive.
+static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad) {
+  const uint64_t stride = L + pad;
+  uint8_t* d_data;
+  CK(hipMalloc(&d_data, stride * (uint64_t)n));
+  const uint64_t segs = (L + 1023) / 1024, thr = segs * (uint64_t)n;
+  hipLaunchKernelGGL(qsmd5_lcg_fill_kernel, dim3((thr + 255) / 256), dim3(256), 0, 0, d_data, stride, L,
+                     12345u, n, segs);
+  std::vector<ChunkDesc> h(n);
+  for (uint32_t i = 0; i < n; ++i) h[i] = {d_data + stride * (uint64_t)i, L};
+  ChunkDesc* d_desc;
+  uint32_t* d_dig;
+  uint64_t* d_st;
+  const uint32_t waves = (n + 63) / 64;
+  CK(hipMalloc(&d_desc, sizeof(ChunkDesc) * n));
+  CK(hipMalloc(&d_dig, 16ull * n));
+  CK(hipMalloc(&d_st, 32ull * waves));
+  CK(hipMemcpy(d_desc, h.data(), sizeof(ChunkDesc) * n, hipMemcpyHostToDevice));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  std::vector<uint64_t> st(4ull * waves);
+  for (int rep = 0; rep <= reps; ++rep) {  // rep 0: warm-up, not reported
+    CK(hipEventRecord(e0, 0));
+    hipLaunchKernelGGL(k_coal_stamped, dim3(waves), dim3(64), 0, 0, d_desc, n, d_dig, d_st);
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    CK(hipMemcpy(st.data(), d_st, st.size() * 8, hipMemcpyDeviceToHost));
+    if (rep == 0) continue;
+    uint64_t r_min = ~0ull, r_max = 0;
+    for (uint32_t w = 0; w < waves; ++w) {
+      r_min = std::min(r_min, st[4 * w + 1]);
+      r_max = std::max(r_max, st[4 * w + 3]);
+    }
+    std::vector<double> clk(waves), start_us(waves), end_us(waves), life_us(waves);
+    double alive = 0;
+    std::vector<double> xcd_end(8, 0.0);
+    for (uint32_t w = 0; w < waves; ++w) {
+      const double dr = (double)(st[4 * w + 3] - st[4 * w + 1]);  // 10 ns ticks
+      clk[w] = dr > 0 ? (double)(st[4 * w + 2] - st[4 * w + 0]) / (dr * 10.0) : 0.0;  // GHz
+      start_us[w] = (st[4 * w + 1] - r_min) * 0.01;
+      end_us[w] = (st[4 * w + 3] - r_min) * 0.01;
+      life_us[w] = dr * 0.01;
+      alive += life_us[w];
+      xcd_end[w % 8] = std::max(xcd_end[w % 8], end_us[w]);
+    }
+    const double span_us = (r_max - r_min) * 0.01;
+    printf("{\"mode\": \"stamps\", \"chains\": %u, \"chunk_KiB\": %llu, \"rep\": %d, \"event_ms\": %.4f, "
+           "\"GBps\": %.1f, \"span_us\": %.1f, \"clock_GHz_p10_p50_p90\": [%.3f, %.3f, %.3f], "
+           "\"start_us_p50_p99_max\": [%.1f, %.1f, %.1f], \"end_us_min_p50_max\": [%.1f, %.1f, %.1f], "
+           "\"life_us_p10_p50_p90\": [%.1f, %.1f, %.1f], \"alive_share\": %.4f, \"xcd_end_us\": [",
+           n, (unsigned long long)(L >> 10), rep, ms, (double)n * L / (ms * 1e-3) / 1e9, span_us,
+           pctl(clk, 0.1), pctl(clk, 0.5), pctl(clk, 0.9), pctl(start_us, 0.5), pctl(start_us, 0.99),
+           pctl(start_us, 1.0), pctl(end_us, 0.0), pctl(end_us, 0.5), pctl(end_us, 1.0), pctl(life_us, 0.1),
+           pctl(life_us, 0.5), pctl(life_us, 0.9), alive / (waves * span_us));
+    for (int x = 0; x < 8; ++x) printf("%s%.1f", x ? ", " : "", xcd_end[x]);
+    printf("]}\n");
+    fflush(stdout);
+  }
+  CK(hipEventDestroy(e0));
+  CK(hipEventDestroy(e1));
+  CK(hipFree(d_st));
+  CK(hipFree(d_dig));
+  CK(hipFree(d_desc));
+  CK(hipFree(d_data));
+}
+
 // ---- 2. MD5 batch kernel -----------------------------------------------------
 static bool g_host_pinned = false;  // "zc" mode: chunks in pinned host memory (zero-copy)
 static uint32_t g_skew = kPcSkewBlocks;  // latency kernel start skew (blocks per lane)
@@ -1609,6 +1707,10 @@ int main(int argc, char** argv) {
     run_coal_probe<1>(262144, 65536, 4352, 3);
     run_coal_probe<2>(262144, 65536, 4352, 3);
     run_coal_probe<0>(8192, 1 << 20, 4352, 3);
+    return 0;
+  }
+  if (!strcmp(mode, "stamps")) {  // round 5: clock vs ramp/tail of the coalesced kernel
+    for (uint64_t kib : {16, 64, 256}) run_stamps(131072, kib << 10, 10, 4352);
     return 0;
   }
   if (!strcmp(mode, "sat")) {
