@@ -179,7 +179,7 @@ struct EventSet {
 // take, so it must not hold Dev::mu (every other batch on this GPU) meanwhile;
 // and jobs of different files (qsfs flushes files from several FUSE threads at
 // once) each read on their own thread, so a GPU keeps up to
-// QSMD5_READ_SLOTS (default 2, at most kMaxReadSlots) of them running side
+// QSMD5_READ_SLOTS (default 4, at most kMaxReadSlots) of them running side
 // by side.  The stream and events are made on first use, the buffers grow
 // with the jobs (HostPinned / DevBuf reserve).
 constexpr int kMaxReadSlots = 8;
@@ -214,7 +214,7 @@ struct Dev {
   std::mutex read_mu;
   std::condition_variable read_cv;
   uint32_t read_busy = 0;  // bit k: slot k has a job
-  int nread_slots = 2;
+  int nread_slots = 4;
   ReadSlot read_slot[kMaxReadSlots];
 };
 

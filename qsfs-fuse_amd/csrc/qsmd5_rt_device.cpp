@@ -132,7 +132,7 @@ static int init_dev(Dev& d, int device) {
       (e = hipEventCreateWithFlags(&d.ev_done, hipEventBlockingSync | hipEventDisableTiming)) !=
           hipSuccess)
     return hip_fail(e, "hipEventCreate");
-  d.nread_slots = (int)std::min<uint64_t>(kMaxReadSlots, std::max<uint64_t>(1, env_u64("QSMD5_READ_SLOTS", 2)));
+  d.nread_slots = (int)std::min<uint64_t>(kMaxReadSlots, std::max<uint64_t>(1, env_u64("QSMD5_READ_SLOTS", 4)));
   if ((e = qsmd5::warm_up(d.compute[0])) != hipSuccess ||
       (e = hipStreamSynchronize(d.compute[0])) != hipSuccess)
     return hip_fail(e, "qsmd5: kernel warm-up (is this a gfx950 GPU?)");
