@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
 #include <chrono>
 #include <vector>
 
@@ -610,22 +611,31 @@ static double run_issue(ukern k, int instr_per_iter, int iters, int threads) {
 // ---- 1b. Stamped coalesced kernel (round 5) ---------------
 // Diagnostic build of qsmd5_batch_coal_kernel: each wave stamps its start and
 // end in shader cycles (s_memtime) and in the 100 MHz constant clock
-// (s_memrealtime) into a buffer of its own that no other code reads; no
-// output is computed from them.  Splits a dispatch's time into the clock the
-// waves ran at and the spread of wave start / end times (ramp and tail).
+// (s_memrealtime), plus where it ran (HW_ID: SIMD, CU, SE; XCC_ID), into a
+// buffer of its own that no other code reads; no output is computed from
+// them.  Splits a dispatch's time into the clock the waves ran at and the
+// spread of wave start / end times, by waves per SIMD.  `extra_lds` bytes of
+// dynamic LDS per workgroup cap the workgroups a CU can hold (160 KiB / LDS
+// per workgroup), which decides how the dispatcher spreads them.
 __global__ __launch_bounds__(64) void k_coal_stamped(const ChunkDesc* __restrict__ chunks, uint32_t n,
                                                      uint32_t* __restrict__ digests, uint64_t* stamps) {
+  extern __shared__ uint32_t pad_lds[];
   const uint64_t c0 = __builtin_amdgcn_s_memtime();
   const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
   batch_coal_body<2, 2>(chunks, nullptr, n, digests);
   const uint64_t c1 = __builtin_amdgcn_s_memtime();
   const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
+  // s_getreg_b32 HW_REG_HW_ID (4) and HW_REG_XCC_ID (20), all 32 bits
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
   if (threadIdx.x == 0) {
-    uint64_t* q = stamps + 4ull * blockIdx.x;
+    uint64_t* q = stamps + 6ull * blockIdx.x;
     q[0] = c0;
     q[1] = r0;
     q[2] = c1;
     q[3] = r1;
+    q[4] = hw;
+    q[5] = xcc | ((uint64_t)pad_lds[0] << 63 >> 63 << 32);  // keeps the dynamic LDS referenced
   }
 }
 
@@ -634,10 +644,10 @@ static double pctl(std::vector<double> v, double q) {
   return v[(size_t)std::min<double>(v.size() - 1, q * (v.size() - 1) + 0.5)];
 }
 
-// One line per launch of n x L (stride L + pad): event ms, the waves' median
-// clock, start and end spread, and the share of (first start .. last end)
-// an average wave is alive.
-static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad) {
+// One line per launch of n x L (stride L + pad): event ms, the waves' clock,
+// start and end spread, the share of (first start .. last end) an average wave
+// is alive, and the waves per SIMD / per CU with each class's mean lifetime.
+static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad, uint32_t extra_lds) {
   const uint64_t stride = L + pad;
   uint8_t* d_data;
   CK(hipMalloc(&d_data, stride * (uint64_t)n));
@@ -652,15 +662,15 @@ static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad) {
   const uint32_t waves = (n + 63) / 64;
   CK(hipMalloc(&d_desc, sizeof(ChunkDesc) * n));
   CK(hipMalloc(&d_dig, 16ull * n));
-  CK(hipMalloc(&d_st, 32ull * waves));
+  CK(hipMalloc(&d_st, 48ull * waves));
   CK(hipMemcpy(d_desc, h.data(), sizeof(ChunkDesc) * n, hipMemcpyHostToDevice));
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  std::vector<uint64_t> st(4ull * waves);
+  std::vector<uint64_t> st(6ull * waves);
   for (int rep = 0; rep <= reps; ++rep) {  // rep 0: warm-up, not reported
     CK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL(k_coal_stamped, dim3(waves), dim3(64), 0, 0, d_desc, n, d_dig, d_st);
+    hipLaunchKernelGGL(k_coal_stamped, dim3(waves), dim3(64), extra_lds, 0, d_desc, n, d_dig, d_st);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -669,32 +679,56 @@ static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad) {
     if (rep == 0) continue;
     uint64_t r_min = ~0ull, r_max = 0;
     for (uint32_t w = 0; w < waves; ++w) {
-      r_min = std::min(r_min, st[4 * w + 1]);
-      r_max = std::max(r_max, st[4 * w + 3]);
+      r_min = std::min(r_min, st[6 * w + 1]);
+      r_max = std::max(r_max, st[6 * w + 3]);
     }
-    std::vector<double> clk(waves), start_us(waves), end_us(waves), life_us(waves);
-    double alive = 0;
-    std::vector<double> xcd_end(8, 0.0);
+    // where each wave ran: (xcc, se, cu) -> CU key; SIMD key adds simd
+    auto cu_key = [&](uint32_t w) {
+      const uint64_t hw = st[6 * w + 4], xcc = st[6 * w + 5] & 0xf;
+      return (xcc << 16) | ((hw >> 8) & 0xff);  // CU_ID [11:8], SH_ID [12], SE_ID [15:13]
+    };
+    auto simd_key = [&](uint32_t w) { return (cu_key(w) << 2) | ((st[6 * w + 4] >> 4) & 3); };
+    std::map<uint64_t, int> per_cu, per_simd;
     for (uint32_t w = 0; w < waves; ++w) {
-      const double dr = (double)(st[4 * w + 3] - st[4 * w + 1]);  // 10 ns ticks
-      clk[w] = dr > 0 ? (double)(st[4 * w + 2] - st[4 * w + 0]) / (dr * 10.0) : 0.0;  // GHz
-      start_us[w] = (st[4 * w + 1] - r_min) * 0.01;
-      end_us[w] = (st[4 * w + 3] - r_min) * 0.01;
-      life_us[w] = dr * 0.01;
-      alive += life_us[w];
-      xcd_end[w % 8] = std::max(xcd_end[w % 8], end_us[w]);
+      ++per_cu[cu_key(w)];
+      ++per_simd[simd_key(w)];
     }
+    std::vector<double> clk(waves), start_us(waves), end_us(waves);
+    double alive = 0;
+    std::map<int, std::pair<double, int>> life_by_simd_load;  // waves on the SIMD -> (sum life, count)
+    for (uint32_t w = 0; w < waves; ++w) {
+      const double dr = (double)(st[6 * w + 3] - st[6 * w + 1]);  // 10 ns ticks
+      clk[w] = dr > 0 ? (double)(st[6 * w + 2] - st[6 * w + 0]) / (dr * 10.0) : 0.0;  // GHz
+      start_us[w] = (st[6 * w + 1] - r_min) * 0.01;
+      end_us[w] = (st[6 * w + 3] - r_min) * 0.01;
+      alive += dr * 0.01;
+      auto& e = life_by_simd_load[per_simd[simd_key(w)]];
+      e.first += dr * 0.01;
+      e.second += 1;
+    }
+    std::map<int, int> cu_hist, simd_hist;
+    for (auto& kv : per_cu) ++cu_hist[kv.second];
+    for (auto& kv : per_simd) ++simd_hist[kv.second];
     const double span_us = (r_max - r_min) * 0.01;
-    printf("{\"mode\": \"stamps\", \"chains\": %u, \"chunk_KiB\": %llu, \"rep\": %d, \"event_ms\": %.4f, "
-           "\"GBps\": %.1f, \"span_us\": %.1f, \"clock_GHz_p10_p50_p90\": [%.3f, %.3f, %.3f], "
-           "\"start_us_p50_p99_max\": [%.1f, %.1f, %.1f], \"end_us_min_p50_max\": [%.1f, %.1f, %.1f], "
-           "\"life_us_p10_p50_p90\": [%.1f, %.1f, %.1f], \"alive_share\": %.4f, \"xcd_end_us\": [",
-           n, (unsigned long long)(L >> 10), rep, ms, (double)n * L / (ms * 1e-3) / 1e9, span_us,
-           pctl(clk, 0.1), pctl(clk, 0.5), pctl(clk, 0.9), pctl(start_us, 0.5), pctl(start_us, 0.99),
-           pctl(start_us, 1.0), pctl(end_us, 0.0), pctl(end_us, 0.5), pctl(end_us, 1.0), pctl(life_us, 0.1),
-           pctl(life_us, 0.5), pctl(life_us, 0.9), alive / (waves * span_us));
-    for (int x = 0; x < 8; ++x) printf("%s%.1f", x ? ", " : "", xcd_end[x]);
-    printf("]}\n");
+    printf("{\"mode\": \"stamps\", \"chains\": %u, \"chunk_KiB\": %llu, \"extra_lds\": %u, \"rep\": %d, "
+           "\"event_ms\": %.4f, \"GBps\": %.1f, \"span_us\": %.1f, \"clock_GHz_p10_p50_p90\": [%.3f, %.3f, %.3f], "
+           "\"start_us_p50_max\": [%.1f, %.1f], \"end_us_min_p50_max\": [%.1f, %.1f, %.1f], "
+           "\"alive_share\": %.4f, \"cus\": %zu, \"simds\": %zu",
+           n, (unsigned long long)(L >> 10), extra_lds, rep, ms, (double)n * L / (ms * 1e-3) / 1e9, span_us,
+           pctl(clk, 0.1), pctl(clk, 0.5), pctl(clk, 0.9), pctl(start_us, 0.5), pctl(start_us, 1.0),
+           pctl(end_us, 0.0), pctl(end_us, 0.5), pctl(end_us, 1.0), alive / (waves * span_us), per_cu.size(),
+           per_simd.size());
+    printf(", \"waves_per_cu_hist\": {");
+    bool first = true;
+    for (auto& kv : cu_hist) printf("%s\"%d\": %d", first ? "" : ", ", kv.first, kv.second), first = false;
+    printf("}, \"waves_per_simd_hist\": {");
+    first = true;
+    for (auto& kv : simd_hist) printf("%s\"%d\": %d", first ? "" : ", ", kv.first, kv.second), first = false;
+    printf("}, \"mean_life_us_by_waves_on_simd\": {");
+    first = true;
+    for (auto& kv : life_by_simd_load)
+      printf("%s\"%d\": %.1f", first ? "" : ", ", kv.first, kv.second.first / kv.second.second), first = false;
+    printf("}}\n");
     fflush(stdout);
   }
   CK(hipEventDestroy(e0));
@@ -1710,7 +1744,10 @@ int main(int argc, char** argv) {
     return 0;
   }
   if (!strcmp(mode, "stamps")) {  // round 5: clock vs ramp/tail of the coalesced kernel
-    for (uint64_t kib : {16, 64, 256}) run_stamps(131072, kib << 10, 10, 4352);
+    // extra LDS per workgroup: 0 (16 KiB static: up to 10 per CU), 4 KiB (20 KiB: 8 per CU,
+    // 2048 workgroups = exactly 8 on each of 256 CUs)
+    for (uint32_t extra : {0u, 4096u})
+      for (uint64_t kib : {64, 256}) run_stamps(131072, kib << 10, 6, 4352, extra);
     return 0;
   }
   if (!strcmp(mode, "sat")) {
