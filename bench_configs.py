@@ -348,10 +348,14 @@ def pool(reps, n=512):
     del t
 
 
-def saturation(reps, L=64 * 1024, pad=4352, n=131072):
+def saturation(reps, L=64 * 1024, pad=4352, n=131072, warm_s=0.5):
     """Throughput regime: 131072 independent chains (one wave per 64, 8 waves per
     CU = one resident round), where the coalesced kernel runs instead of the
-    latency kernel.  Reports the median and best of >= 10 launches."""
+    latency kernel.  Reports the median and best of >= 10 launches, timed after
+    >= warm_s seconds of untimed launches: the chip raises its clock over the
+    first tens of ms of load (1.6 -> 1.9 GHz in the per-wave stamps,
+    profiles/r05_stamps.jsonl), and without this warm-up a 10-launch series of
+    short launches is timed mostly inside that ramp (round 5)."""
     import torch
     import qsmd5
     from oracle_util import md5_many
@@ -365,6 +369,14 @@ def saturation(reps, L=64 * 1024, pad=4352, n=131072):
     desc = desc.cuda()
     dig = torch.zeros((n, 16), dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()
+    import time
+    t_warm, warm = time.time(), 0
+    while time.time() - t_warm < warm_s:
+        for _ in range(4):
+            qsmd5.hash_device(desc.data_ptr(), dig.data_ptr(), n, stream=s.cuda_stream,
+                              flags=qsmd5.FLAG_ALIGNED16)
+        warm += 4
+        torch.cuda.synchronize()
     reps = max(reps, 10)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(reps + 1)]
@@ -384,7 +396,7 @@ def saturation(reps, L=64 * 1024, pad=4352, n=131072):
         n, L // 1024, pad, ["v1", "pc", "coal", "pc2"][qsmd5.kernel_choice(n, qsmd5.FLAG_ALIGNED16)]),
         "GiBps": round(n * L / GiB / (med * 1e-3), 1), "GBps": round(gbs, 1),
         "frac_of_hbm_peak": round(gbs / HBM_PEAK_GBS, 4), "kernel_ms_median": round(med, 3),
-        "kernel_ms_best": round(best, 3), "launches": reps,
+        "kernel_ms_best": round(best, 3), "launches": reps, "warmup_launches": warm,
         "best_frac_of_hbm_peak": round(n * L / (best * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         "parity": "ok (64 sampled chunks vs oracle)" if ok else "FAIL"})
     del t

@@ -67,11 +67,19 @@ def main(rnd):
     co_kib = fetch_kib(sat_pmc, "qsmd5_batch_coal_kernel")
     trace = [r for r in rows(os.path.join(RAW, "sat", "sat_kernel_trace.csv"))
              if r["Kernel_Name"].startswith("qsmd5_batch_coal_kernel")]
+    trace.sort(key=lambda r: int(r["Start_Timestamp"]))
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace]
-    half = len(durs) // 2
+    # Since round 5 each size runs untimed warm-up launches first (a time
+    # budget, so their count varies): split the two sizes by magnitude (4x
+    # apart) and keep each size's last 11 dispatches, the timed ones.
+    def split(vals, keep=11):
+        cut = (min(vals) * max(vals)) ** 0.5
+        return [v for v in vals if v < cut][-keep:], [v for v in vals if v >= cut][-keep:]
+    kib64, kib256 = split(co_kib)
+    d64, d256 = split(durs)
     out = []
-    for label, L, kib, d in (("131072x64KiB", 65536, co_kib[:len(co_kib) // 2], durs[:half]),
-                             ("131072x256KiB", 262144, co_kib[len(co_kib) // 2:], durs[half:])):
+    for label, L, kib, d in (("131072x64KiB", 65536, kib64, d64),
+                             ("131072x256KiB", 262144, kib256, d256)):
         a = 131072 * L
         b = statistics.median(kib) * 1024.0 * factor
         med = statistics.median(d)

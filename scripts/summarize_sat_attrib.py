@@ -49,7 +49,7 @@ def pmc(name):
         d = out.setdefault(int(r["Dispatch_Id"]), {})
         d[r["Counter_Name"]] = float(r["Counter_Value"])
         d["ns"] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    disp = [out[k] for k in sorted(out)][1:]  # the first launch is the warm-up
+    disp = [out[k] for k in sorted(out)][-(LAUNCHES - 1):]  # the timed launches (warm-up ones first)
     return disp
 
 
@@ -96,11 +96,17 @@ def main():
     a = my - b * mx
     trace = rows(one("trace/**/sat_kernel_trace.csv"))
     coal = sorted((r for r in trace if r["Kernel_Name"].startswith(KERNEL)), key=lambda r: int(r["Start_Timestamp"]))
-    trace_ms = []
-    for i in range(0, len(coal), LAUNCHES):
-        grp = coal[i + 1:i + LAUNCHES]
-        trace_ms.append(round(statistics.median((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-                                                for r in grp), 4))
+    # consecutive dispatches of one size form a run (sizes are 2x apart); the
+    # last LAUNCHES - 1 of each run are the timed ones
+    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in coal]
+    runs, cur = [], [dur[0]]
+    for d in dur[1:]:
+        if d > 1.5 * statistics.median(cur) or d < statistics.median(cur) / 1.5:
+            runs.append(cur)
+            cur = []
+        cur.append(d)
+    runs.append(cur)
+    trace_ms = [round(statistics.median(r[-(LAUNCHES - 1):]), 4) for r in runs]
     s64, s256 = size_line("sat64", 64 * 1024), size_line("sat256", 256 * 1024)
     # The 64 KiB dispatch against 1/4 of the 256 KiB one (same bytes per chain
     # ratio): how many of its cycles each mechanism explains.
