@@ -22,6 +22,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 RAW = os.path.join(ROOT, "gpurun_out", "r05_sat")
+TAG = sys.argv[1] if len(sys.argv) > 1 else ""  # suffix of the profiles/ names (e.g. "_warm")
 PROF = os.path.join(ROOT, "profiles")
 KERNEL = "qsmd5_batch_coal_kernel"
 N = 131072
@@ -134,11 +135,11 @@ def main():
                     "the 64 KiB VALU rate",
         },
     }
-    json.dump(out, open(os.path.join(PROF, "r05_sat_attribution.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(PROF, "r05_sat_attribution%s.json" % TAG), "w"), indent=1)
     for name in ("sat64_a", "sat64_b", "sat256_a", "sat256_b"):
         shutil.copy(one("pmc_%s/**/pmc_counter_collection.csv" % name),
-                    os.path.join(PROF, "r05_sat_pmc_%s.csv" % name))
-    shutil.copy(one("trace/**/sat_kernel_stats.csv"), os.path.join(PROF, "r05_sat_kernel_stats.csv"))
+                    os.path.join(PROF, "r05_sat_pmc_%s%s.csv" % (name, TAG)))
+    shutil.copy(one("trace/**/sat_kernel_stats.csv"), os.path.join(PROF, "r05_sat_kernel_stats%s.csv" % TAG))
     json.dump(out, sys.stdout, indent=1)
     print()
 
