@@ -96,17 +96,19 @@ def main():
     b = sum((x - mx) * (y - my) for x, y in zip(xs, ys)) / sum((x - mx) ** 2 for x in xs)
     a = my - b * mx
     trace = rows(one("trace/**/sat_kernel_trace.csv"))
-    coal = sorted((r for r in trace if r["Kernel_Name"].startswith(KERNEL)), key=lambda r: int(r["Start_Timestamp"]))
-    # consecutive dispatches of one size form a run (sizes are 2x apart); the
-    # last LAUNCHES - 1 of each run are the timed ones
-    dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in coal]
-    runs, cur = [], [dur[0]]
-    for d in dur[1:]:
-        if d > 1.5 * statistics.median(cur) or d < statistics.median(cur) / 1.5:
-            runs.append(cur)
+    # each size fills its chunks (qsmd5_lcg_fill_kernel) before its launches:
+    # the fills separate the sizes' runs; the last LAUNCHES - 1 of a run are
+    # the timed launches (warm-up ones come first)
+    runs, cur = [], []
+    for r in sorted(trace, key=lambda r: int(r["Start_Timestamp"])):
+        if r["Kernel_Name"].startswith("qsmd5_lcg_fill"):
+            if cur:
+                runs.append(cur)
             cur = []
-        cur.append(d)
-    runs.append(cur)
+        elif r["Kernel_Name"].startswith(KERNEL):
+            cur.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+    if cur:
+        runs.append(cur)
     trace_ms = [round(statistics.median(r[-(LAUNCHES - 1):]), 4) for r in runs]
     s64, s256 = size_line("sat64", 64 * 1024), size_line("sat256", 256 * 1024)
     # The 64 KiB dispatch against 1/4 of the 256 KiB one (same bytes per chain
