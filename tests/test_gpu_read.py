@@ -221,3 +221,45 @@ def test_concurrent_files_read_slots(slots):
     assert r["gpu_waves"] == 4 and r["pool_free_after"] == 5
     print("QSMD5_READ_SLOTS=%s: 4 files x 64 parts in %.3f s (%.2f GiB/s)"
           % (slots, r["wall_s_runs"][-1], 4 * 640 / 1024.0 / r["wall_s_runs"][-1]))
+
+
+def test_concurrent_reads_contend_for_slots():
+    """Eight threads, each pulling its own ragged batch (0 B .. 3 MiB chunks,
+    staging budgets from 1 MiB to the default) through qsmd5_hash_read at
+    once, against the default 4 read slots: half of them wait for a slot
+    while the others run side by side.  Every digest equals the oracle's on
+    the same bytes and every reader sees the read contract (each chunk's
+    windows in order, every byte once)."""
+    import random
+    import threading
+    from oracle_util import md5_many
+    rng = random.Random(2025)
+    jobs = []
+    for j in range(8):
+        lens = [rng.choice([0, 1, 55, 64, 4096, 65536, 1 << 20, 3 << 20, rng.randrange(1, 3 << 20)])
+                for _ in range(rng.randrange(1, 96))]
+        pos, offs = 0, []
+        for L in lens:
+            offs.append(pos)
+            pos += L
+        host = _host_lcg(1, max(pos, 1), 9000 + j)
+        chunks = [(host.ctypes.data + o, L) for o, L in zip(offs, lens)]
+        jobs.append({"lens": lens, "host": host, "chunks": chunks, "rd": Reader(chunks),
+                     "staging": rng.choice([0, 1 * MiB, 4 * MiB, 32 * MiB])})
+    errors = []
+
+    def work(job):
+        try:
+            job["got"] = qsmd5.hash_read(job["lens"], job["rd"], staging_bytes=job["staging"], flags=GPU)
+        except Exception as e:  # carried to the main thread
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(job,)) for job in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errors and all(not t.is_alive() for t in th), errors
+    for job in jobs:
+        assert job["got"] == md5_many(job["chunks"])
+        job["rd"].check_contract()
