@@ -300,12 +300,14 @@ QSMD5_API int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t
  * the CPU, asking for every byte again from offset 0.  It may call other qsmd5
  * entry points (not qsmd5_shutdown).  lens[i] < 2^38.  Routed like
  * qsmd5_hash_batch_ex (flags: QSMD5_FLAG_GPU_ONLY / _CPU_ONLY /
- * _REF_TRUNCATE32); on the GPU the first bound GPU hashes it.  Calls from
- * different threads (files flushed at once) run side by side on the GPU, each
- * with its own stream and staging, up to QSMD5_READ_SLOTS at a time (default
- * 4, at most 8; each slot holds up to 2 x staging_bytes of pinned host memory
- * and staging_bytes of HBM, taken on first use); a further call waits for one
- * of them to return. */
+ * _REF_TRUNCATE32).  Calls from different threads (files flushed at once)
+ * run side by side, each with its own stream and staging, up to
+ * QSMD5_READ_SLOTS per GPU at a time (default 4, at most 8; each slot holds
+ * up to 2 x staging_bytes of pinned host memory and staging_bytes of HBM,
+ * taken on first use); a further call waits for a slot.  One bound GPU
+ * hashes a whole call: the one with the fewest such calls in flight (the
+ * first on a tie), so with QSMD5_DEVICES binding several, files flushed at
+ * once spread over the GPUs. */
 typedef uint64_t (*qsmd5_read_fn)(void* user, size_t chunk, uint64_t offset, uint64_t len, void* dst);
 QSMD5_API int qsmd5_hash_read(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* user,
                               uint64_t staging_bytes, uint8_t (*digests)[16], int flags);

@@ -72,35 +72,69 @@ int poll_event(hipEvent_t ev, const char* what) {
   }
 }
 
-// A read slot of `r` for this job (qsmd5_rt.h ReadSlot): the first free one,
-// or wait until a job returns one.  Its stream and events are made on first use.
+// A read slot for this job (qsmd5_rt.h ReadSlot) and the bound GPU it is on.
+// With several GPUs bound (QSMD5_DEVICES), the job goes to the one with the
+// fewest jobs in flight for its slots (the first on a tie), so files flushed
+// at once spread over the node's GPUs and one file at a time stays on the
+// primary.  The GPU and slot are taken together under that GPU's lock, so two
+// jobs starting at once never both pick a GPU whose last slot only one of
+// them can have; when every slot is busy, the job waits on the least-loaded
+// GPU.  The slot's stream and events are made on first use.
 struct SlotLease {
-  Dev& r;
+  Dev* r = nullptr;
   int k = -1;
-  explicit SlotLease(Dev& dev) : r(dev) {
-    std::unique_lock<std::mutex> lk(r.read_mu);
-    r.read_cv.wait(lk, [&] {
-      for (int i = 0; i < r.nread_slots; ++i)
-        if (!(r.read_busy & (1u << i))) {
-          k = i;
+  size_t index = 0;  // the GPU's place in rt().devs
+  SlotLease() {
+    Runtime& R = rt();
+    const size_t n = R.devs.size();
+    std::vector<std::pair<double, size_t>> by_load(n);
+    for (size_t i = 0; i < n; ++i) {
+      Dev* d = R.devs[i];
+      std::lock_guard<std::mutex> lk(d->read_mu);
+      by_load[i] = {(double)__builtin_popcount(d->read_busy) / (double)std::max(1, d->nread_slots), i};
+    }
+    std::stable_sort(by_load.begin(), by_load.end(),
+                     [](const std::pair<double, size_t>& x, const std::pair<double, size_t>& y) {
+                       return x.first < y.first;
+                     });
+    for (const auto& c : by_load)
+      if (take(*R.devs[c.second], c.second, false)) return;
+    take(*R.devs[by_load[0].second], by_load[0].second, true);
+  }
+  // A free slot of d (waiting for one if `wait`); false if none was free.
+  bool take(Dev& d, size_t i, bool wait) {
+    std::unique_lock<std::mutex> lk(d.read_mu);
+    auto free_slot = [&] {
+      for (int s = 0; s < d.nread_slots; ++s)
+        if (!(d.read_busy & (1u << s))) {
+          k = s;
           return true;
         }
       return false;
-    });
-    r.read_busy |= 1u << k;
+    };
+    if (wait) d.read_cv.wait(lk, free_slot);
+    else if (!free_slot()) return false;
+    d.read_busy |= 1u << k;
+    r = &d;
+    index = i;
+    return true;
   }
   ~SlotLease() {
     {
-      std::lock_guard<std::mutex> lk(r.read_mu);
-      r.read_busy &= ~(1u << k);
+      std::lock_guard<std::mutex> lk(r->read_mu);
+      r->read_busy &= ~(1u << k);
     }
-    r.read_cv.notify_one();
+    r->read_cv.notify_one();
   }
   SlotLease(const SlotLease&) = delete;
   SlotLease& operator=(const SlotLease&) = delete;
+  // The slot on its GPU (made current: the stream and buffers live there).
   int ready(ReadSlot** out) {
-    ReadSlot& rs = r.read_slot[k];
-    hipError_t e;
+    hipError_t e = hipSetDevice(r->device);  // guarded() restores the caller's device
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    if (rt().devs.size() > 1 && env_u64("QSMD5_TRACE", 0))  // diagnostics (tests/test_gpu_multi.py)
+      fprintf(stderr, "qsmd5 read: job on context %zu (GPU %d)\n", index, r->device);
+    ReadSlot& rs = r->read_slot[k];
     if (!rs.stream && (e = hipStreamCreateWithFlags(&rs.stream, hipStreamNonBlocking)) != hipSuccess) {
       rs.stream = nullptr;
       return hip_fail(e, "hipStreamCreate");
@@ -115,8 +149,8 @@ struct SlotLease {
   }
 };
 
-int gpu_read(Dev& r, ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
-  SlotLease lease(r);
+int gpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
+  SlotLease lease;
   ReadSlot* slot = nullptr;
   if (int rc = lease.ready(&slot)) return rc;
   ReadSlot& rs = *slot;
@@ -293,7 +327,7 @@ int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* u
       sticky = !strcmp(inj, "sticky");
       rc = fail(-EIO, "qsmd5: injected GPU fault (QSMD5_INJECT_GPU_FAULT)");
     } else {
-      rc = gpu_read(primary(), J, staging, digests);
+      rc = gpu_read(J, staging, digests);
     }
   }
   if (rc == 0) {

@@ -154,3 +154,39 @@ print("parts-ok")
     shards = [l for l in out.stderr.splitlines() if l.startswith("qsmd5 shard:")]
     assert any("context 1 (GPU 0) takes" in l and not l.endswith("takes 0 chunks") for l in shards), \
         "\n".join(shards)
+
+
+def test_concurrent_read_jobs_spread_over_bound_gpus():
+    """Pull-driven batches (qsmd5_hash_read) from four threads at once, with
+    two bound contexts (QSMD5_DEVICES=0,0) and one read slot each: the jobs
+    go to the context with the fewest in flight, so both take some, and every
+    digest equals the oracle's."""
+    script = r'''
+import ctypes, threading
+import qsmd5
+from oracle_util import lcg_bytes, md5_many
+MiB = 1 << 20
+jobs = []
+for j in range(4):
+    lens = [MiB + 4099 * i for i in range(24)]
+    bufs = [lcg_bytes(3000 + 100 * j + i, L) for i, L in enumerate(lens)]
+    jobs.append({"lens": lens, "bufs": bufs})
+def reader(bufs):
+    def read(chunk, off, n, dst):
+        ctypes.memmove(dst, ctypes.addressof(bufs[chunk]) + off, n)
+        return n
+    return read
+def work(job):
+    job["got"] = qsmd5.hash_read(job["lens"], reader(job["bufs"]), staging_bytes=4 * MiB,
+                                 flags=qsmd5.FLAG_GPU_ONLY)
+th = [threading.Thread(target=work, args=(job,)) for job in jobs]
+for t in th: t.start()
+for t in th: t.join()
+for job in jobs:
+    assert job["got"] == md5_many([(b, L) for b, L in zip(job["bufs"], job["lens"])])
+print("read-spread-ok")
+'''
+    out = _run(script, QSMD5_DEVICES="0,0", QSMD5_TRACE="1", QSMD5_READ_SLOTS="1")
+    assert out.returncode == 0 and "read-spread-ok" in out.stdout, out.stdout + out.stderr[-4000:]
+    ctx = [l.split("context ")[1].split()[0] for l in out.stderr.splitlines() if l.startswith("qsmd5 read: job")]
+    assert len(ctx) == 4 and set(ctx) == {"0", "1"}, ctx
