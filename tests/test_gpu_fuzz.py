@@ -139,3 +139,50 @@ def test_random_stream_updates(pools, seed):
         h.update((base + off if L else 0, L))
     want = md5_many([(pools["host"].ctypes.data + start, pos - start)])[0]
     assert h.finalize().digest() == want, (seed, [(L, k) for _, L, k in pieces])
+
+
+N_READ = max(16, N_BATCH // 4)
+
+
+@pytest.mark.parametrize("seed", range(N_READ))
+def test_random_read_batches(pools, seed):
+    """Pull-driven batches (qsmd5_hash_read, round 5): random lengths (edges,
+    0 B .. ~2 MiB), random chunk counts and staging budgets from 64 KiB (one
+    row of a window per chunk, many groups) to 64 MiB, read from the pinned,
+    registered or pageable pool, sometimes from several threads at once (the
+    read slots).  Every digest against the oracle on the same bytes."""
+    import threading
+    rng = random.Random(5000 + seed)
+    jobs = []
+    for _ in range(rng.choice([1, 1, 2, 3, 6])):
+        n = rng.choice([1, 2, 17, 64, 65, 200])
+        kind = rng.choice(["pinned", "reg", "host"])
+        lens, offs = [], []
+        for _ in range(n):
+            L = _length(rng)
+            lens.append(L)
+            offs.append(rng.randrange(POOL - L))
+        jobs.append({"lens": lens, "offs": offs, "kind": kind,
+                     "staging": rng.choice([0, 64 << 10, 1 << 20, 4 << 20, 64 << 20])})
+
+    def run(job):
+        base = pools[job["kind"]].ctypes.data
+
+        def read(chunk, off, length, dst):
+            ctypes.memmove(dst, base + job["offs"][chunk] + off, length)
+            return length
+        try:
+            job["got"] = qsmd5.hash_read(job["lens"], read, staging_bytes=job["staging"],
+                                         flags=qsmd5.FLAG_GPU_ONLY)
+        except Exception as e:  # reported below
+            job["err"] = repr(e)
+
+    th = [threading.Thread(target=run, args=(j,)) for j in jobs]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    for j in jobs:
+        assert "err" not in j, (seed, j["err"])
+        want = md5_many([(pools["host"].ctypes.data + o, L) for o, L in zip(j["offs"], j["lens"])])
+        assert j["got"] == want, (seed, len(j["lens"]), j["staging"], j["kind"])
