@@ -743,7 +743,11 @@ __device__ __forceinline__ void coal_fast_group(uint32_t (&st)[4], const uint8_t
   }
 }
 
-template <int kTB, int kBufs, bool kImm = false>
+// kPrioEpoch (ubench only; 0 in every product kernel): every 2^kPrioEpoch
+// tiles of the fast region, a wave sets its issue priority to
+// (epoch ^ WAVE_ID) & 1, so the two waves of a SIMD take turns at the
+// higher priority instead of the older one finishing first (round 5 stamps).
+template <int kTB, int kBufs, bool kImm = false, int kPrioEpoch = 0>
 __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ chunks,
                                                 const uint32_t* __restrict__ order, uint32_t n,
                                                 uint32_t* __restrict__ digests) {
@@ -822,6 +826,11 @@ __device__ __forceinline__ void batch_coal_body(const ChunkDesc* __restrict__ ch
     for (int i = 0; i < kS; ++i)
       gp[i] = src[i] + kTB * 64u + (piece[i] >> 2) * 64u + (piece[i] & 3u) * 16u;
     for (; tl + (uint32_t)kU < fast_tiles; tl += (uint32_t)kU) {
+      if constexpr (kPrioEpoch > 0) {
+        const uint32_t wave_id = __builtin_amdgcn_s_getreg((3 << 11) | 4) & 0xfu;  // HW_ID[3:0]
+        if (((tl >> kPrioEpoch) ^ wave_id) & 1u) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
       coal_fast_group<0, kU, kTB, kS, kCPI, kImm>(st, gp, tile_buf, lane, rswz);
       if constexpr (kImm) {
 #pragma unroll

@@ -617,12 +617,13 @@ static double run_issue(ukern k, int instr_per_iter, int iters, int threads) {
 // spread of wave start / end times, by waves per SIMD.  `extra_lds` bytes of
 // dynamic LDS per workgroup cap the workgroups a CU can hold (160 KiB / LDS
 // per workgroup), which decides how the dispatcher spreads them.
+template <int kPrioEpoch>
 __global__ __launch_bounds__(64) void k_coal_stamped(const ChunkDesc* __restrict__ chunks, uint32_t n,
                                                      uint32_t* __restrict__ digests, uint64_t* stamps) {
   extern __shared__ uint32_t pad_lds[];
   const uint64_t c0 = __builtin_amdgcn_s_memtime();
   const uint64_t r0 = __builtin_amdgcn_s_memrealtime();
-  batch_coal_body<2, 2>(chunks, nullptr, n, digests);
+  batch_coal_body<2, 2, false, kPrioEpoch>(chunks, nullptr, n, digests);
   const uint64_t c1 = __builtin_amdgcn_s_memtime();
   const uint64_t r1 = __builtin_amdgcn_s_memrealtime();
   // s_getreg_b32 HW_REG_HW_ID (4) and HW_REG_XCC_ID (20), all 32 bits
@@ -647,7 +648,7 @@ static double pctl(std::vector<double> v, double q) {
 // One line per launch of n x L (stride L + pad): event ms, the waves' clock,
 // start and end spread, the share of (first start .. last end) an average wave
 // is alive, and the waves per SIMD / per CU with each class's mean lifetime.
-static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad, uint32_t extra_lds) {
+static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad, uint32_t extra_lds, int prio = 0) {
   const uint64_t stride = L + pad;
   uint8_t* d_data;
   CK(hipMalloc(&d_data, stride * (uint64_t)n));
@@ -670,7 +671,12 @@ static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad, uint32_t 
   std::vector<uint64_t> st(6ull * waves);
   for (int rep = 0; rep <= reps; ++rep) {  // rep 0: warm-up, not reported
     CK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL(k_coal_stamped, dim3(waves), dim3(64), extra_lds, 0, d_desc, n, d_dig, d_st);
+    if (prio == 0)
+      hipLaunchKernelGGL(k_coal_stamped<0>, dim3(waves), dim3(64), extra_lds, 0, d_desc, n, d_dig, d_st);
+    else if (prio == 2)
+      hipLaunchKernelGGL(k_coal_stamped<2>, dim3(waves), dim3(64), extra_lds, 0, d_desc, n, d_dig, d_st);
+    else
+      hipLaunchKernelGGL(k_coal_stamped<4>, dim3(waves), dim3(64), extra_lds, 0, d_desc, n, d_dig, d_st);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -710,11 +716,11 @@ static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad, uint32_t 
     for (auto& kv : per_cu) ++cu_hist[kv.second];
     for (auto& kv : per_simd) ++simd_hist[kv.second];
     const double span_us = (r_max - r_min) * 0.01;
-    printf("{\"mode\": \"stamps\", \"chains\": %u, \"chunk_KiB\": %llu, \"extra_lds\": %u, \"rep\": %d, "
+    printf("{\"mode\": \"stamps\", \"prio_epoch\": %d, \"chains\": %u, \"chunk_KiB\": %llu, \"extra_lds\": %u, \"rep\": %d, "
            "\"event_ms\": %.4f, \"GBps\": %.1f, \"span_us\": %.1f, \"clock_GHz_p10_p50_p90\": [%.3f, %.3f, %.3f], "
            "\"start_us_p50_max\": [%.1f, %.1f], \"end_us_min_p50_max\": [%.1f, %.1f, %.1f], "
            "\"alive_share\": %.4f, \"cus\": %zu, \"simds\": %zu",
-           n, (unsigned long long)(L >> 10), extra_lds, rep, ms, (double)n * L / (ms * 1e-3) / 1e9, span_us,
+           prio, n, (unsigned long long)(L >> 10), extra_lds, rep, ms, (double)n * L / (ms * 1e-3) / 1e9, span_us,
            pctl(clk, 0.1), pctl(clk, 0.5), pctl(clk, 0.9), pctl(start_us, 0.5), pctl(start_us, 1.0),
            pctl(end_us, 0.0), pctl(end_us, 0.5), pctl(end_us, 1.0), alive / (waves * span_us), per_cu.size(),
            per_simd.size());
@@ -731,6 +737,19 @@ static void run_stamps(uint32_t n, uint64_t L, int reps, uint64_t pad, uint32_t 
     printf("}}\n");
     fflush(stdout);
   }
+  // the last launch's digests of 64 chains spread over the batch, against the oracle
+  int bad = 0;
+  std::vector<uint8_t> buf(L);
+  uint8_t got[16], want[16];
+  for (uint32_t k = 0; k < 64; ++k) {
+    const uint32_t i = (uint32_t)(((uint64_t)k * 2039u) % n);
+    CK(hipMemcpy(buf.data(), d_data + stride * (uint64_t)i, L, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(got, d_dig + 4ull * i, 16, hipMemcpyDeviceToHost));
+    oracle_md5(buf.data(), L, want);
+    bad += memcmp(got, want, 16) != 0;
+  }
+  printf("{\"mode\": \"stamps_parity\", \"prio_epoch\": %d, \"chunk_KiB\": %llu, \"checked\": 64, \"bad\": %d}\n",
+         prio, (unsigned long long)(L >> 10), bad);
   CK(hipEventDestroy(e0));
   CK(hipEventDestroy(e1));
   CK(hipFree(d_st));
@@ -1741,6 +1760,13 @@ int main(int argc, char** argv) {
     run_coal_probe<1>(262144, 65536, 4352, 3);
     run_coal_probe<2>(262144, 65536, 4352, 3);
     run_coal_probe<0>(8192, 1 << 20, 4352, 3);
+    return 0;
+  }
+  if (!strcmp(mode, "prio")) {  // round 5: alternating issue priority, A/B/A/B after a warm-up
+    run_stamps(131072, 64 << 10, 20, 4352, 0, 0);  // warm-up series (its lines are reported too)
+    for (int round = 0; round < 2; ++round)
+      for (int prio : {0, 2, 4})
+        for (uint64_t kib : {64, 256}) run_stamps(131072, kib << 10, 5, 4352, 0, prio);
     return 0;
   }
   if (!strcmp(mode, "stamps")) {  // round 5: clock vs ramp/tail of the coalesced kernel
