@@ -184,7 +184,12 @@ struct WaveStats {
 };
 
 struct PrehashOptions {
-  bool pipeline = true;        // gather + hash the next wave while this one uploads
+  // Gather + hash the next wave on a helper thread while this one uploads.
+  // The helper calls read(), so read() must not wait for a lock the calling
+  // thread holds: a synchronous File::Flush keeps the file's recursive_mutex
+  // through the upload (File.cpp:619, 641-643) and every ReadNoLoad takes it
+  // (File.cpp:310) -- pass false there ("The file's lock").
+  bool pipeline = true;
   size_t max_wave = 0;         // parts per wave at most (0: as many as free buffers)
   bool upload_releases = false;  // true: a buffer is upload()'s once upload() returns, and
                                  // its completion handler releases it (an async
@@ -410,6 +415,7 @@ struct StagedOptions {
   // and each larger wave is pre-hashed while the smaller one before it uploads.
   size_t first_wave_parts = 0;
   bool pipeline = true;        // pre-hash the next wave on a helper thread while this one uploads
+                               // (read_range then runs there too: PrehashOptions::pipeline)
   bool upload_releases = false;  // as PrehashOptions::upload_releases
   int flags = 0;               // qsmd5_hash_read flags (QSMD5_FLAG_GPU_ONLY / _CPU_ONLY)
   std::function<bool()> should_continue;  // as PrehashOptions::should_continue (thread-safe)
@@ -488,7 +494,8 @@ std::vector<std::string> md5_parts_read(const std::vector<qsmd5_part>& parts, Re
 // parts, pool, upload: as upload_parts_prehashed.  read_range(file_offset,
 // len, char* dst) -> bytes copied: File::ReadNoLoad(off, len, dst).first; with
 // `pipeline` it is also called from the helper thread pre-hashing the next
-// wave, so it must be thread-safe (ReadNoLoad locks the file).  Stats: waves =
+// wave, so it must be thread-safe (ReadNoLoad locks the file) and must not
+// wait for a lock this thread holds (PrehashOptions::pipeline).  Stats: waves =
 // pre-hash calls, gpu_waves / cpu_waves by their backend, hash_s = time in
 // them (reads included), upload_s = the upload loop (its own reads included),
 // wait_s = upload time spent waiting for a pre-hash (hashing not hidden).

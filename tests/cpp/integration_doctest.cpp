@@ -13,18 +13,29 @@
 // handed on carries the MD5 of its bytes, cancelled or unsent parts are marked
 // failed, and every buffer is back in the pool.
 //
-// usage: integration_doctest <file_bytes> <part_bytes> <pool_buffers> <cancel_after|-1>
+// usage: integration_doctest <file_bytes> <part_bytes> <pool_buffers> <cancel_after|-1> [flush]
+//   flush: async (default: File::Flush submitted the upload and returned, no
+//   lock held), sync (the flushing thread holds the file's lock through the
+//   upload and sets the flag, as File::Flush's synchronous branch with the
+//   binding's addition), sync_unflagged (the negative control: the lock held,
+//   the flag not set -- a helper thread's read waits forever; the watchdog
+//   exits 3).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -116,9 +127,13 @@ struct TransferHandle {  // locked like the real one (TransferHandle.h:159-162):
   }
 };
 
-struct PagedFile {  // File::ReadNoLoad: bytes [off, off + len) into dst
+struct PagedFile {  // File::ReadNoLoad: bytes [off, off + len) into dst, under the file's lock
   std::vector<char> bytes;
+  mutable std::recursive_mutex m_mutex;  // File's (File.h); ReadNoLoad locks it (File.cpp:310)
+  bool m_flushingUnderLock = false;      // the binding's added flag
+  bool IsFlushingUnderLock() const { return m_flushingUnderLock; }
   std::pair<size_t, int> ReadNoLoad(uint64_t off, uint64_t len, char* dst) const {
+    std::lock_guard<std::recursive_mutex> lock(m_mutex);
     memcpy(dst, bytes.data() + off, len);
     return std::make_pair((size_t)len, 0);
   }
@@ -195,11 +210,29 @@ int main(int argc, char** argv) {
   uint64_t largest = 0;
   for (const auto& p : plan) largest = std::max<uint64_t>(largest, p.size);
 
+  const std::string flush = argc > 5 ? argv[5] : "async";
   Uploader up;
   up.rm = make_shared<ResourceManager>(pool_n, largest);
   auto handle = make_shared<TransferHandle>();
   handle->cancel_after = cancel_after;
-  up.DoMultiPartUpload(handle, &file, queued, plan);
+  std::atomic<bool> done{false};
+  std::thread watchdog([&] {
+    for (int i = 0; i < 300 && !done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    if (!done.load()) {
+      printf("{\"deadlock\": true, \"flush\": \"%s\"}\n", flush.c_str());
+      fflush(stdout);
+      _exit(3);
+    }
+  });
+  {
+    std::unique_lock<std::recursive_mutex> held(file.m_mutex, std::defer_lock);
+    if (flush != "async") held.lock();  // File::Flush's lock_guard (File.cpp:619)
+    file.m_flushingUnderLock = flush == "sync";
+    up.DoMultiPartUpload(handle, &file, queued, plan);
+    file.m_flushingUnderLock = false;
+  }
+  done.store(true);
+  watchdog.join();
 
   int bad = 0;
   auto expect = [&](bool ok, const char* what) {
@@ -222,7 +255,7 @@ int main(int argc, char** argv) {
   expect(failed.size() == n - want_sent, "every part not sent is marked failed");
   for (uint16_t id : failed) expect(!up.client->sent.count(id), "a failed part was not sent");
   expect(up.rm->Free() == pool_n, "every buffer is back in the pool");
-  printf("{\"parts\": %zu, \"sent\": %zu, \"failed\": %zu, \"pool_free\": %zu, \"bad\": %d}\n", n,
+  printf("{\"parts\": %zu, \"sent\": %zu, \"failed\": %zu, \"pool_free\": %zu, \"bad\": %d, \"deadlock\": false}\n", n,
          up.client->sent.size(), failed.size(), up.rm->Free(), bad);
   return bad ? 1 : 0;
 }

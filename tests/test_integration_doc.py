@@ -53,17 +53,35 @@ def doctest_exe(tmp_path_factory):
     return exe
 
 
+@pytest.mark.parametrize("flush", ["async", "sync"])
 @pytest.mark.parametrize("cancel_after", [-1, 0, 1, 7, 12, 100],
                          ids=["whole_file", "cancelled_first", "after_1", "after_7", "after_12", "never"])
-def test_binding_as_printed(doctest_exe, cancel_after):
-    # 12 x 4 MiB + 1234 B: 13 parts, the last two averaged (PrepareUpload, :517-542)
+def test_binding_as_printed(doctest_exe, cancel_after, flush):
+    """async: File::Flush handed the upload to the executor (no lock held);
+    sync: the flushing thread holds the file's lock through the upload
+    (single-thread mode, File::Truncate) and the binding must not read from
+    its helper thread.  12 x 4 MiB + 1234 B: 13 parts, the last two averaged
+    (PrepareUpload, :517-542); 66 parts at 2 MiB, more than one wave."""
     env = dict(os.environ, QSMD5_BACKEND="cpu")
-    out = subprocess.run([doctest_exe, str(12 * 4 * MiB + 1234), str(4 * MiB), "5", str(cancel_after)],
+    for fsz, psz, nparts in ((12 * 4 * MiB + 1234, 4 * MiB, 13), (132 * MiB, 2 * MiB, 66)):
+        out = subprocess.run([doctest_exe, str(fsz), str(psz), "5", str(cancel_after), flush],
+                             env=env, capture_output=True, text=True, timeout=120)
+        assert out.returncode == 0, out.stdout + out.stderr[-3000:]
+        r = json.loads(out.stdout.strip().splitlines()[-1])
+        sent = nparts if cancel_after < 0 else min(nparts, cancel_after)
+        assert r == {"parts": nparts, "sent": sent, "failed": nparts - sent, "pool_free": 5, "bad": 0,
+                     "deadlock": False}, r
+
+
+def test_sync_flush_without_the_flag_deadlocks(doctest_exe):
+    """The negative control: the flushing thread holds the file's lock, as
+    File::Flush's synchronous branch does, but the binding is not told -- its
+    pipeline's helper thread blocks in ReadNoLoad while the flushing thread
+    waits for it.  The doctest's watchdog reports the deadlock (exit 3)."""
+    env = dict(os.environ, QSMD5_BACKEND="cpu")
+    out = subprocess.run([doctest_exe, str(132 * MiB), str(2 * MiB), "5", "-1", "sync_unflagged"],
                          env=env, capture_output=True, text=True, timeout=120)
-    assert out.returncode == 0, out.stdout + out.stderr[-3000:]
-    r = json.loads(out.stdout.strip().splitlines()[-1])
-    sent = 13 if cancel_after < 0 else min(13, cancel_after)
-    assert r == {"parts": 13, "sent": sent, "failed": 13 - sent, "pool_free": 5, "bad": 0}, r
+    assert out.returncode == 3 and '"deadlock": true' in out.stdout, (out.returncode, out.stdout)
 
 
 def test_log_sink_binding_as_printed(tmp_path):
