@@ -52,6 +52,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstring>
 #include <condition_variable>
 #include <exception>
 #include <functional>
@@ -180,6 +181,7 @@ struct WaveStats {
   bool stopped = false;  // should_continue() said stop (TransferHandle::ShouldContinue)
   size_t gpu_waves = 0, cpu_waves = 0, split_waves = 0;  // by qsmd5_last_backend of each wave
   size_t widest_wave = 0;
+  size_t rehashed = 0;   // upload_parts_staged: parts re-hashed from their buffer (source_changed)
   double gather_s = 0, hash_s = 0, upload_s = 0, wait_s = 0, wall_s = 0;
 };
 
@@ -419,6 +421,15 @@ struct StagedOptions {
   bool upload_releases = false;  // as PrehashOptions::upload_releases
   int flags = 0;               // qsmd5_hash_read flags (QSMD5_FLAG_GPU_ONLY / _CPU_ONLY)
   std::function<bool()> should_continue;  // as PrehashOptions::should_continue (thread-safe)
+  // The pre-hash reads the file before the upload loop reads each part again
+  // into its buffer: a write in between would send a Content-MD5 that does not
+  // match the part (the reference hashes the very buffer it sends,
+  // QSClient.cpp:369-371).  source_changed() is asked after each part lands
+  // in its buffer; true (the file was written since the pre-hash began: the
+  // binding compares File's write version) re-hashes that part from the
+  // buffer (qsmd5_hash_one), so the digest always matches the bytes sent.
+  // Empty: the file does not change during the upload.
+  std::function<bool()> source_changed;
 };
 
 namespace detail {
@@ -570,6 +581,12 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
           if (got != p.size)
             throw std::runtime_error("short read of part " + std::to_string(p.part_number) + ": " +
                                      std::to_string(got) + " of " + std::to_string(p.size) + " bytes");
+          if (opt.source_changed && opt.source_changed()) {
+            uint8_t d[16];
+            detail::check(qsmd5_hash_one(Pool::data(b), p.size, d), "qsmd5_hash_one");
+            std::memcpy(&cur.dig[16 * k], d, 16);
+            ++st.rehashed;
+          }
           upload(p, b, detail::hex(&cur.dig[16 * k]));
         } catch (...) {
           pool.release(b);  // not handed over

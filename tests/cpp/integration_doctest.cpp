@@ -13,13 +13,14 @@
 // handed on carries the MD5 of its bytes, cancelled or unsent parts are marked
 // failed, and every buffer is back in the pool.
 //
-// usage: integration_doctest <file_bytes> <part_bytes> <pool_buffers> <cancel_after|-1> [flush]
+// usage: integration_doctest <file_bytes> <part_bytes> <pool_buffers> <cancel_after|-1> [flush] [write_after]
 //   flush: async (default: File::Flush submitted the upload and returned, no
 //   lock held), sync (the flushing thread holds the file's lock through the
 //   upload and sets the flag, as File::Flush's synchronous branch with the
 //   binding's addition), sync_unflagged (the negative control: the lock held,
 //   the flag not set -- a helper thread's read waits forever; the watchdog
-//   exits 3).
+//   exits 3).  write_after: once that many parts went out, the file is
+//   written (the next part to go out changes) as by another descriptor.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -132,6 +133,13 @@ struct PagedFile {  // File::ReadNoLoad: bytes [off, off + len) into dst, under 
   mutable std::recursive_mutex m_mutex;  // File's (File.h); ReadNoLoad locks it (File.cpp:310)
   bool m_flushingUnderLock = false;      // the binding's added flag
   bool IsFlushingUnderLock() const { return m_flushingUnderLock; }
+  std::atomic<uint64_t> m_writeVersion{0};  // the binding's added write counter
+  uint64_t GetWriteVersion() const { return m_writeVersion.load(); }
+  void Write(uint64_t off, const char* src, size_t len) {  // File::Write, under the lock
+    std::lock_guard<std::recursive_mutex> lock(m_mutex);
+    memcpy(bytes.data() + off, src, len);
+    ++m_writeVersion;
+  }
   std::pair<size_t, int> ReadNoLoad(uint64_t off, uint64_t len, char* dst) const {
     std::lock_guard<std::recursive_mutex> lock(m_mutex);
     memcpy(dst, bytes.data() + off, len);
@@ -146,7 +154,8 @@ struct IOStream {  // a view of the pooled buffer's first `len` bytes (StreamBuf
 };
 
 struct Client {
-  std::map<uint16_t, std::string> sent;  // part id -> Content-MD5 the SDK got
+  std::map<uint16_t, std::string> sent;   // part id -> Content-MD5 the SDK got
+  std::map<uint16_t, std::string> truth;  // part id -> MD5 of the bytes the SDK got
 };
 typedef int UploadResult;
 
@@ -170,6 +179,9 @@ static void DebugError(const std::string& m) { fprintf(stderr, "DebugError: %s\n
 struct Uploader {
   shared_ptr<ResourceManager> rm;
   shared_ptr<Client> client = make_shared<Client>();
+  PagedFile* writer = nullptr;  // another descriptor writing the file mid-upload
+  int write_after = -1;         // ... once this many parts went out
+  uint64_t write_off = 0;
   shared_ptr<ResourceManager> GetBufferManager() { return rm; }
   shared_ptr<Client> GetClient() { return client; }
   // QSTransferManager::MultipleUploadWrapper (:721-727) with the digest argument
@@ -177,6 +189,15 @@ struct Uploader {
                                      const shared_ptr<IOStream>& stream) {
     if (!stream->buf || stream->len != part->size) return -1;
     client->sent[part->id] = part->GetContentMD5();
+    uint8_t d[16];
+    char hex[33];
+    if (qsmd5_hash_one(stream->buf->data(), stream->len, d)) return -1;
+    qsmd5_hex(d, hex);
+    client->truth[part->id] = hex;
+    if (writer && (int)client->sent.size() == write_after) {
+      const char junk[] = "written by another descriptor during the upload";
+      writer->Write(write_off, junk, sizeof(junk));
+    }
     return 0;
   }
 
@@ -212,6 +233,13 @@ int main(int argc, char** argv) {
 
   const std::string flush = argc > 5 ? argv[5] : "async";
   Uploader up;
+  up.write_after = argc > 6 ? atoi(argv[6]) : -1;
+  if (up.write_after >= 0) {
+    up.writer = &file;
+    // the next part to go out: already pre-hashed (its wave is the one uploading)
+    const qsmd5_part& next = plan[std::min<size_t>(up.write_after, plan.size() - 1)];
+    up.write_off = next.offset + next.size / 2;
+  }
   up.rm = make_shared<ResourceManager>(pool_n, largest);
   auto handle = make_shared<TransferHandle>();
   handle->cancel_after = cancel_after;
@@ -244,12 +272,14 @@ int main(int argc, char** argv) {
   const size_t want_sent = cancel_after < 0 ? n : std::min<size_t>(n, (size_t)cancel_after);
   expect(up.client->sent.size() == want_sent, "parts handed to the SDK");
   for (const auto& kv : up.client->sent) {
+    expect(kv.second == up.client->truth[kv.first], "a part's Content-MD5 is the MD5 of the bytes sent");
+    if (up.write_after >= 0) continue;
     const Part& p = *queued[kv.first];
     uint8_t d[16];
     char hex[33];
     if (qsmd5_hash_one(file.bytes.data() + p.begin, p.size, d)) return 1;
     qsmd5_hex(d, hex);
-    expect(kv.second == hex, "a part's Content-MD5 is the MD5 of its bytes");
+    expect(kv.second == hex, "a part's Content-MD5 is the MD5 of the file's bytes");
   }
   std::set<uint16_t> failed(handle->failed.begin(), handle->failed.end());
   expect(failed.size() == n - want_sent, "every part not sent is marked failed");

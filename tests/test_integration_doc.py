@@ -73,6 +73,43 @@ def test_binding_as_printed(doctest_exe, cancel_after, flush):
                      "deadlock": False}, r
 
 
+@pytest.mark.parametrize("flush", ["async", "sync"])
+def test_write_during_the_upload_rehashes_the_part(doctest_exe, flush):
+    """Another descriptor writes the next part to go out after 3 parts went
+    out: the stored digest of that part no longer matches its bytes, so the
+    binding (source_changed over File's write counter) re-hashes it from its
+    buffer; every Content-MD5 the SDK gets is the MD5 of the bytes it gets."""
+    env = dict(os.environ, QSMD5_BACKEND="cpu")
+    out = subprocess.run([doctest_exe, str(132 * MiB), str(2 * MiB), "5", "-1", flush, "3"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr[-3000:]
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["sent"] == 66 and r["bad"] == 0, r
+
+
+def test_write_during_the_upload_negative_control(tmp_path):
+    """The same binding with its source_changed line taken out: the part
+    written mid-upload goes out with the pre-hash's stale digest, and the
+    doctest sees it (exit 1)."""
+    adapter, loop = snippet_pieces()
+    lines = [ln for ln in loop.splitlines() if ln.startswith("opt.source_changed")]
+    assert len(lines) == 1, loop
+    (tmp_path / "adapter.inc").write_text(adapter)
+    (tmp_path / "loop.inc").write_text(loop.replace(lines[0], "// " + lines[0]))
+    exe = str(tmp_path / "integration_doctest_nc")
+    subprocess.check_call([
+        "g++", "-std=c++17", "-O1", "-Wall", "-Wno-unused-variable", "-Wno-unused-but-set-variable",
+        '-DINTEGRATION_ADAPTER="%s"' % (tmp_path / "adapter.inc"), '-DINTEGRATION_LOOP="%s"' % (tmp_path / "loop.inc"),
+        os.path.join(ROOT, "tests", "cpp", "integration_doctest.cpp"),
+        "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(ROOT, "qsfs-fuse_amd", "host"),
+        "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5", "-lpthread",
+        "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-o", exe])
+    env = dict(os.environ, QSMD5_BACKEND="cpu")
+    out = subprocess.run([exe, str(132 * MiB), str(2 * MiB), "5", "-1", "async", "3"],
+                         env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 1 and "MD5 of the bytes sent" in out.stderr, (out.returncode, out.stderr[-2000:])
+
+
 def test_sync_flush_without_the_flag_deadlocks(doctest_exe):
     """The negative control: the flushing thread holds the file's lock, as
     File::Flush's synchronous branch does, but the binding is not told -- its
