@@ -581,6 +581,10 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
           if (got != p.size)
             throw std::runtime_error("short read of part " + std::to_string(p.part_number) + ": " +
                                      std::to_string(got) + " of " + std::to_string(p.size) + " bytes");
+          if (stop_requested()) {  // asked again after the read, as the reference (:645)
+            pool.release(b);
+            break;
+          }
           if (opt.source_changed && opt.source_changed()) {
             uint8_t d[16];
             detail::check(qsmd5_hash_one(Pool::data(b), p.size, d), "qsmd5_hash_one");
