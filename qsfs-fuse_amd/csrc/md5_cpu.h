@@ -44,6 +44,13 @@ void md5_mb16(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[1
 void md5_mb32(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16], MbPull pull,
               void* ctx);
 
+// Resumable multi-buffer form (pull-driven batches, qsmd5_rt_read.cpp): job i
+// continues state[i] over nblocks[i] whole 64-B blocks at ptrs[i], 16 jobs at
+// a time in the lanes; each state is written back when its job ends, with no
+// padding (the running Ctx finishes the message).  Call only if
+// mb16_available().
+void md5_mb16_blocks(uint32_t (*state)[4], const uint8_t* const* ptrs, const uint64_t* nblocks, size_t count);
+
 // Streaming state: the MD5 class (update()* then final()), any piece sizes.
 struct Ctx {
   uint32_t h[4] = {kIV[0], kIV[1], kIV[2], kIV[3]};

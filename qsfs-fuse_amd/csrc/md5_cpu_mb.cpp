@@ -198,9 +198,78 @@ QS_AVX512 void runG(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*
   }
 }
 
+// The resumable form (md5_mb16_blocks): job i continues state[i] over
+// nblocks[i] whole blocks at ptrs[i]; 16 lanes run in lockstep, a lane whose
+// job is done takes the next one, and each state is written back as its job
+// ends (no padding: the caller's running context finishes the message).
+QS_AVX512 void run_blocks(uint32_t (*state)[4], const uint8_t* const* ptrs, const uint64_t* nblocks,
+                          size_t count) {
+  constexpr int L = 16;
+  const uint8_t* p[L];
+  uint64_t left[L];
+  size_t idx[L];
+  bool busy[L];
+  alignas(64) uint32_t s[4][L];
+  for (int l = 0; l < L; ++l) {
+    p[l] = kZeroBlock;
+    left[l] = 0;
+    busy[l] = false;
+  }
+  __m512i S[4];
+  for (int k = 0; k < 4; ++k) S[k] = _mm512_setzero_si512();
+  size_t next = 0;
+  for (;;) {
+    // refill idle lanes with the next job's state
+    for (int k = 0; k < 4; ++k) _mm512_store_si512((void*)s[k], S[k]);
+    for (int l = 0; l < L; ++l)
+      while (!busy[l] && next < count) {
+        const size_t i = next++;
+        if (nblocks[i] == 0) continue;  // nothing to run: the state stands
+        busy[l] = true;
+        idx[l] = i;
+        p[l] = ptrs[i];
+        left[l] = nblocks[i];
+        for (int k = 0; k < 4; ++k) s[k][l] = state[i][k];
+      }
+    for (int k = 0; k < 4; ++k) S[k] = _mm512_load_si512((const void*)s[k]);
+    __mmask16 live = 0;
+    uint64_t run = ~0ull;
+    for (int l = 0; l < L; ++l)
+      if (busy[l]) {
+        live |= (__mmask16)(1u << l);
+        run = left[l] < run ? left[l] : run;
+      }
+    if (!live) return;
+    for (uint64_t j = 0; j < run; ++j) {
+      __m512i x[1][16];
+      const uint8_t* const(&pg)[16] = *reinterpret_cast<const uint8_t* const(*)[16]>(p);
+      load_transpose(x[0], pg);
+      __m512i v[4][1];
+      for (int k = 0; k < 4; ++k) v[k][0] = S[k];
+      stepsG<1, 0>(v, x);
+      for (int k = 0; k < 4; ++k) S[k] = _mm512_mask_add_epi32(S[k], live, S[k], v[k][0]);
+      for (int l = 0; l < L; ++l)
+        if (busy[l]) p[l] += 64;
+    }
+    for (int k = 0; k < 4; ++k) _mm512_store_si512((void*)s[k], S[k]);
+    for (int l = 0; l < L; ++l) {
+      if (!busy[l]) continue;
+      left[l] -= run;
+      if (left[l]) continue;
+      for (int k = 0; k < 4; ++k) state[idx[l]][k] = s[k][l];
+      busy[l] = false;
+      p[l] = kZeroBlock;
+    }
+  }
+}
+
 }  // namespace
 
 bool mb16_available() { return __builtin_cpu_supports("avx512f"); }
+
+void md5_mb16_blocks(uint32_t (*state)[4], const uint8_t* const* ptrs, const uint64_t* nblocks, size_t count) {
+  run_blocks(state, ptrs, nblocks, count);
+}
 
 void md5_mb16(const uint8_t* const* ptrs, const uint64_t* lens, uint8_t (*out)[16], MbPull pull,
               void* ctx) {

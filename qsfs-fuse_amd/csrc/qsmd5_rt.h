@@ -586,6 +586,7 @@ double cpu_efficiency();
 void note_cpu_batch(double priced_ms, double measured_ms);
 double cpu_priced_ms(const qsmd5_chunk* chunks, size_t n, int flags);
 double cpu_model_ms(uint64_t longest, uint64_t total);  // scalar chains, idle host
+double read_lanes_model_ms(uint64_t longest, uint64_t total, size_t n);  // < 0: not priced
 bool cpu_is_faster(const qsmd5_chunk* chunks, size_t n, int flags);
 std::vector<uint32_t> plan_split(const qsmd5_chunk* chunks, size_t n, int flags);
 int cpu_batch(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int flags,

@@ -23,6 +23,8 @@
 // while step s copies and hashes.  The reads are the bound: a column kernel of
 // 512 chains x 508 KiB runs in ~4 ms, the copy in ~5 ms, while one thread
 // gathers the 254 MiB in ~20 ms (the page cache's memcpy).
+#include <array>
+
 #include "qsmd5_rt.h"
 
 namespace qsmd5 {
@@ -38,6 +40,7 @@ struct ReadJob {
   std::vector<uint64_t> sorted;  // len[order[k]]
   uint64_t total = 0;
   bool short_read = false;       // the caller's read came back short: not a GPU failure
+  double read_s = 0;             // time in the caller's reads (the read-rate estimate)
 };
 
 // The window of column j of group g for its `active` live lanes, lane k at
@@ -203,7 +206,10 @@ int gpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
       if (step >= 2)  // the copy that last read this region (step - 2) has finished
         if (int rc = poll_event(rs.copied[reg], "qsmd5_hash_read: staging copy")) return drain(rc);
       const size_t act = ReadPlan::active(J.sorted, g, j);
-      if (int rc = fill_window(J, g, j, act, host)) return drain(rc);
+      const auto r0 = std::chrono::steady_clock::now();
+      const int frc = fill_window(J, g, j, act, host);
+      J.read_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - r0).count();
+      if (frc) return drain(frc);
       if (int rc = hip(hipMemcpyAsync(dstage, host, act * g.stride, hipMemcpyHostToDevice, s),
                        "hipMemcpyAsync H2D"))
         return drain(rc);
@@ -222,45 +228,180 @@ int gpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
   return 0;
 }
 
-// The CPU backend of a pull-driven batch: the same windows into a host buffer,
-// each window's rows folded into their chunks' running contexts (md5_cpu.h
-// Ctx) on up to cpu_threads() threads.
+// Whether the CPU backend runs a window of `act` rows on T threads in the
+// AVX-512 lanes (md5_mb16_blocks): as cpu_batch decides, at least 2 rows per
+// thread (a lane's chain runs at ~0.6x a scalar chain), QSMD5_CPU_MB=0: never.
+bool read_lanes(size_t act, size_t T) {
+  return act >= 2 * T && env_u64("QSMD5_CPU_MB", 1) && qsmd5::cpu::mb16_available();
+}
+
+// The CPU backend of a pull-driven batch: the same windows, double-buffered
+// like the GPU's: the calling thread reads window s + 1 (the caller's reads
+// stay on its thread) while worker threads fold window s's rows into their
+// chunks' running contexts (md5_cpu.h Ctx) -- 16 rows at a time per thread in
+// the AVX-512 lanes where read_lanes says so (the rows' whole blocks continue
+// their chunks' states; a final column's last len % 64 bytes go through the
+// Ctx), else one row at a time.  *hash_ms: the workers' wall time, for the
+// load feedback.
 int cpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16], double* hash_ms) {
+  using clock = std::chrono::steady_clock;
   const size_t n = J.len.size();
   const ReadPlan P = plan_read(J.sorted, staging);
   uint64_t region = 0;
   for (const ReadGroup& g : P.groups) region = std::max<uint64_t>(region, g.count * g.stride);
-  std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[std::max<uint64_t>(region, 1)]);
+  std::unique_ptr<uint8_t[]> buf(new (std::nothrow) uint8_t[2 * std::max<uint64_t>(region, 1)]);
   if (!buf) return fail(-ENOMEM, "qsmd5_hash_read: host staging allocation failed");
   std::vector<qsmd5::cpu::Ctx> ctx(n);
-  for (const ReadGroup& g : P.groups)
-    for (uint32_t j = 0; j < g.ncols; ++j) {
-      const size_t act = ReadPlan::active(J.sorted, g, j);
-      if (int rc = fill_window(J, g, j, act, buf.get())) return rc;
-      const auto t0 = std::chrono::steady_clock::now();  // the hashing, not the reads
-      std::atomic<size_t> next{0};
-      auto work = [&]() noexcept {
-        for (size_t k; (k = next.fetch_add(1)) < act;) {
-          const uint32_t c = J.order[g.first + k];
-          const uint64_t w = ReadPlan::col_bytes(g, J.len[c], j);
-          if (w) ctx[c].update(buf.get() + k * g.stride, w);
-        }
-      };
-      const size_t T = std::min<size_t>({cpu_threads(), act, (size_t)std::max<uint64_t>(1, act * g.W >> 20)});
-      std::vector<std::thread> th;
-      for (size_t t = 1; t < T; ++t) {
-        try {
-          th.emplace_back(work);
-        } catch (...) {
-          break;  // fewer helpers: this thread takes the rest
-        }
+
+  // One window's hashing: rows [0, act) of group g, column j, at `base`.
+  struct Window {
+    const ReadGroup* g = nullptr;
+    uint32_t j = 0;
+    size_t act = 0, T = 1;
+    bool lanes = false;
+    const uint8_t* base = nullptr;
+  };
+  auto row_scalar = [&](const Window& w, size_t k) {
+    const uint32_t c = J.order[w.g->first + k];
+    const uint64_t b = ReadPlan::col_bytes(*w.g, J.len[c], w.j);
+    if (b) ctx[c].update(w.base + k * w.g->stride, b);
+  };
+  // lanes: thread t takes rows t, t + T, ... (lengths fall with k, so each
+  // thread gets a like share of long and short rows)
+  auto rows_lanes = [&](const Window& w, size_t t) {
+    std::vector<std::array<uint32_t, 4>> st;
+    std::vector<const uint8_t*> ptr;
+    std::vector<uint64_t> nb;
+    std::vector<size_t> rows;
+    for (size_t k = t; k < w.act; k += w.T) {
+      const uint32_t c = J.order[w.g->first + k];
+      const uint64_t b = ReadPlan::col_bytes(*w.g, J.len[c], w.j);
+      if (!b) continue;
+      if (ctx[c].tail_len || b < 64) {  // a partial block pending: the Ctx's own path
+        ctx[c].update(w.base + k * w.g->stride, b);
+        continue;
       }
-      work();
-      for (auto& t : th) t.join();
-      *hash_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      st.push_back({ctx[c].h[0], ctx[c].h[1], ctx[c].h[2], ctx[c].h[3]});
+      ptr.push_back(w.base + k * w.g->stride);
+      nb.push_back(b >> 6);
+      rows.push_back(k);
     }
+    if (!rows.empty())
+      qsmd5::cpu::md5_mb16_blocks(reinterpret_cast<uint32_t(*)[4]>(st.data()), ptr.data(), nb.data(),
+                                  rows.size());
+    for (size_t r = 0; r < rows.size(); ++r) {
+      const size_t k = rows[r];
+      const uint32_t c = J.order[w.g->first + k];
+      const uint64_t b = ReadPlan::col_bytes(*w.g, J.len[c], w.j);
+      for (int q = 0; q < 4; ++q) ctx[c].h[q] = st[r][q];
+      ctx[c].total += nb[r] << 6;
+      if (b & 63) ctx[c].update(w.base + k * w.g->stride + (nb[r] << 6), b & 63);
+    }
+  };
+  // The window in flight on the workers; finish() joins them (and runs on
+  // this thread any share a worker could not be started for).
+  Window cur;
+  std::vector<std::thread> th;
+  std::vector<uint8_t> started;  // per worker slot: a thread runs it
+  std::atomic<size_t> next{0};
+  // the hashing's own wall time (not the wait for the next window's reads):
+  // launch to the last worker's end
+  clock::time_point t_start;
+  std::atomic<int64_t> t_end_ns{0};
+  auto stamp_end = [&] {
+    const int64_t ns = std::chrono::duration_cast<std::chrono::nanoseconds>(clock::now() - t_start).count();
+    int64_t cur_ns = t_end_ns.load();
+    while (ns > cur_ns && !t_end_ns.compare_exchange_weak(cur_ns, ns)) {
+    }
+  };
+  auto work = [&](const Window& w, size_t t) noexcept {
+    if (w.lanes) rows_lanes(w, t);
+    else
+      for (size_t k; (k = next.fetch_add(1)) < w.act;) row_scalar(w, k);
+    stamp_end();
+  };
+  auto finish = [&] {
+    for (auto& t : th) t.join();
+    th.clear();
+    if (cur.g) {
+      for (size_t t = 0; t < cur.T; ++t)
+        if (!started[t]) work(cur, t);
+      *hash_ms += (double)t_end_ns.load() * 1e-6;
+    }
+    cur = Window();
+  };
+  auto launch = [&](const Window& w) {
+    cur = w;
+    next.store(0);
+    t_end_ns.store(0);
+    started.assign(w.T, 0);
+    t_start = clock::now();
+    for (size_t t = 0; t < w.T; ++t) {
+      try {
+        th.emplace_back(work, std::cref(cur), t);
+        started[t] = 1;
+      } catch (...) {
+        break;  // finish() runs the rest on this thread
+      }
+    }
+  };
+  size_t step = 0;
+  for (const ReadGroup& g : P.groups)
+    for (uint32_t j = 0; j < g.ncols; ++j, ++step) {
+      uint8_t* host = buf.get() + (step & 1) * region;
+      const size_t act = ReadPlan::active(J.sorted, g, j);
+      // this region was last hashed two steps back, and finish() below waited for it
+      const auto r0 = clock::now();
+      const int rc = fill_window(J, g, j, act, host);
+      J.read_s += std::chrono::duration<double>(clock::now() - r0).count();
+      finish();  // window s - 1: its rows are folded, its region is free
+      if (rc) return rc;
+      Window w;
+      w.g = &g;
+      w.j = j;
+      w.act = act;
+      w.T = std::min<size_t>({cpu_threads(), act, (size_t)std::max<uint64_t>(1, act * g.W >> 20)});
+      w.lanes = read_lanes(act, w.T);
+      w.base = host;
+      launch(w);
+    }
+  finish();
   for (size_t c = 0; c < n; ++c) ctx[c].final(digests[c]);
   return 0;
+}
+
+// The caller's read rate (bytes per second of its read callbacks), averaged
+// over recent jobs of >= 64 MiB (a new job weighs 1/2); before the first such
+// job, QSMD5_READ_GIBS or 12 GiB/s (one thread's memcpy out of a page cache,
+// as qsfs's ReadNoLoad).  Both backends overlap the reads with the hashing,
+// so a job's wall time is about max(reads, hashing): routing compares the two
+// backends on that, and a tie goes to the GPU (the CPU's threads are busy for
+// it, the GPU's not).
+std::atomic<uint64_t> g_read_gibs_bits{0};
+
+double read_gibs() {
+  const double env = env_gibs("QSMD5_READ_GIBS");
+  if (env > 0) return env;
+  const uint64_t bits = g_read_gibs_bits.load(std::memory_order_relaxed);
+  if (!bits) return 12.0;
+  double v;
+  memcpy(&v, &bits, sizeof(v));
+  return v;
+}
+
+void note_read_rate(const ReadJob& J) {
+  if (J.total < (64ull << 20) || J.read_s <= 0) return;
+  const double sample = (double)J.total / J.read_s / kGiB;
+  const uint64_t old_bits = g_read_gibs_bits.load(std::memory_order_relaxed);
+  double v = sample;
+  if (old_bits) {
+    double old;
+    memcpy(&old, &old_bits, sizeof(old));
+    v = 0.5 * old + 0.5 * sample;
+  }
+  uint64_t bits;
+  memcpy(&bits, &v, sizeof(bits));
+  g_read_gibs_bits.store(bits, std::memory_order_relaxed);
 }
 
 void log_read(const char* backend, const char* reason, const ReadJob& J) {
@@ -299,6 +440,12 @@ int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* u
   for (size_t k = 0; k < n; ++k) J.sorted[k] = J.len[J.order[k]];
   const uint64_t staging = staging_bytes ? staging_bytes
                                          : env_u64("QSMD5_READ_STAGING_BYTES", kDefaultReadStaging);
+  // idle-host CPU time of this batch: 16 lanes per thread where cpu_read will
+  // use them and they are priced, else scalar chains
+  auto cpu_read_model_ms = [&]() {
+    const double lanes = read_lanes_model_ms(longest, J.total, n);
+    return lanes >= 0 ? lanes : cpu_model_ms(longest, J.total);
+  };
   auto on_cpu = [&](const char* reason) {
     log_read("cpu", reason, J);
     double hash_ms = 0;
@@ -307,16 +454,19 @@ int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* u
       t_last_backend = QSMD5_BACKEND_CPU;
       g_cpu_batches.fetch_add(1);
       g_cpu_chunks.fetch_add(n);
-      note_cpu_batch(cpu_model_ms(longest, J.total), hash_ms);  // scalar chains, as cpu_read runs them
+      note_cpu_batch(cpu_read_model_ms(), hash_ms);  // as cpu_read runs them
+      note_read_rate(J);
     }
     return rc;
   };
   if (b == kCpu) return on_cpu("forced");
   if (b == kAuto) {
     if (g_gpu_lost.load()) return on_cpu("gpu-lost");
-    // the reads cost the same on either backend: price the hashing alone,
-    // as for a batch of host chunks of these lengths
-    if (cpu_est_ms(longest, J.total) < gpu_est_ms(longest, J.total)) return on_cpu("size");
+    // price the hashing as for a batch of host chunks of these lengths
+    const double read_ms = 1e3 * (double)J.total / kGiB / read_gibs();
+    if (std::max(read_ms, cpu_read_model_ms() / cpu_efficiency()) <
+        std::max(read_ms, gpu_est_ms(longest, J.total)))
+      return on_cpu("size");
   }
   log_read("gpu", b == kGpu ? "forced" : "size", J);
   int rc = ensure_init();
@@ -334,6 +484,7 @@ int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* u
     t_last_backend = QSMD5_BACKEND_GPU;
     g_gpu_batches.fetch_add(1);
     g_gpu_chunks.fetch_add(n);
+    note_read_rate(J);
     return 0;
   }
   // Forced GPU: no fallback.  A short read or -EINVAL is the caller's, not the GPU's.

@@ -469,6 +469,21 @@ static bool lanes_priced(const qsmd5_chunk* chunks, size_t n, int flags) {
 static double lanes_est_ms(double rate, double lanes, uint64_t longest, uint64_t total, double T) {
   return 1e3 * std::max((double)longest / (rate / lanes), (double)total / (T * rate)) / kGiB;
 }
+// The pull-driven CPU path (qsmd5_rt_read.cpp cpu_read) runs 16 lanes per
+// thread where it has at least 2 rows per thread: its idle-host model, or a
+// negative value where the lanes are not priced (QSMD5_ROUTE_LANES=0), not
+// available, or the batch too narrow for them.
+double read_lanes_model_ms(uint64_t longest, uint64_t total, size_t n) {
+  const size_t T = std::min<size_t>(cpu_threads(), std::max<size_t>(n, 1));
+  if (!env_u64("QSMD5_ROUTE_LANES", 1) || !env_u64("QSMD5_CPU_MB", 1) || !qsmd5::cpu::mb16_available() ||
+      n < 2 * T)
+    return -1.0;
+  const CpuRates& c = cpu_rates();
+  const double r16 = c.lane16 > 0 ? c.lane16 : c.lane_thread;
+  if (r16 <= 0) return -1.0;
+  return 1e3 * std::max((double)longest / (r16 / 16.0), (double)total / ((double)T * r16)) / kGiB;
+}
+
 static double lanes_model_ms(uint64_t longest, uint64_t total, size_t n) {
   const CpuRates& c = cpu_rates();
   const double T = (double)std::min<size_t>(cpu_threads(), std::max<size_t>(n, 1));

@@ -142,3 +142,53 @@ def test_read_auto_mode_without_gpu_falls_back(monkeypatch):
     got = qsmd5.hash_read(lens, rec)
     assert got == md5_many([(b, L) for b, L in zip(bufs, lens)])
     assert qsmd5.last_backend() == qsmd5.BACKEND_CPU
+
+
+@pytest.mark.parametrize("threads", ["1", "2", "4"])
+@pytest.mark.parametrize("staging", [256 << 10, 4 * MiB, 0])
+def test_read_lanes_and_scalar_agree(monkeypatch, threads, staging):
+    """Round 5: with AVX-512 the CPU backend runs each window 16 rows at a time
+    per thread in the vector lanes (md5_mb16_blocks continues every row's
+    chunk state over its whole blocks; a final column's tail goes through the
+    running context).  Lanes (QSMD5_CPU_MB=1) and scalar rows (=0) give the
+    oracle's digests on ragged lengths, at 1, 2 and 4 threads and budgets
+    that force many groups, and keep the read contract."""
+    monkeypatch.setenv("QSMD5_CPU_THREADS", threads)
+    rng = random.Random(int(threads) * 31 + staging)
+    lens = [0, 1, 63, 64, 65, 127, 128, 4096, 65536, 65537, MiB, 2 * MiB + 63]
+    lens += [rng.randrange(0, 2 * MiB) for _ in range(60)]
+    rng.shuffle(lens)
+    for mb in ("1", "0"):
+        monkeypatch.setenv("QSMD5_CPU_MB", mb)
+        _case(lens, staging, seed=400 + int(threads))
+
+
+def test_read_routing_compares_wall_times(monkeypatch):
+    """Round 5: auto routes a pull-driven batch by its wall time on each
+    backend, max(the caller's reads, the hashing), since both overlap the
+    reads with the hashing.  With reads priced fast (QSMD5_READ_GIBS=50), 8 x
+    10 MiB prices to the CPU lanes (~23 ms) against one GPU chain (~85 ms);
+    with reads priced slow (0.5 GiB/s) both backends are read-bound, the tie
+    goes to the GPU (whose hashing leaves the host's cores free) -- here,
+    without a GPU, that attempt falls back to the CPU.  The log carries the
+    decision."""
+    if qsmd5.device_count() > 0:
+        pytest.skip("GPU present: the slow-read case would really run on it")
+    if "avx512f" not in open("/proc/cpuinfo").read():
+        pytest.skip("host without AVX-512F: the lanes are never priced")
+    for k, v in (("QSMD5_BACKEND", "auto"), ("QSMD5_CPU_THREADS", "4"), ("QSMD5_GPU_CHAIN_GIBS", "0.119"),
+                 ("QSMD5_CPU_LOAD_FEEDBACK", "0"), ("QSMD5_ROUTE_LANES", "1")):
+        monkeypatch.setenv(k, v)
+    lines = []
+    qsmd5.set_log_callback(lambda level, text: lines.append(text))
+    try:
+        lens = [10 * MiB] * 8
+        bufs = [lcg_bytes(77 + i, L) for i, L in enumerate(lens)]
+        want_md5 = md5_many([(b, L) for b, L in zip(bufs, lens)])
+        for gibs, want in (("50", "backend=cpu reason=size"), ("0.5", "backend=gpu reason=size")):
+            monkeypatch.setenv("QSMD5_READ_GIBS", gibs)
+            del lines[:]
+            assert qsmd5.hash_read(lens, Recorder(bufs, lens)) == want_md5  # auto: no flags
+            assert any(want in l and "(read)" in l for l in lines), (gibs, lines)
+    finally:
+        qsmd5.set_log_callback(None)
