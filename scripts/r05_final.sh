@@ -9,3 +9,5 @@ cd "$R"
 bash scripts/r05_suite.sh "${1:-final}" || exit 1
 cd "$R"
 bash scripts/profile_round.sh
+cd "$R"
+bash scripts/r05_staged_sweep.sh 2> "$R/gpurun_out/r05_staged_sweep.err"

@@ -13,7 +13,7 @@ OUT=gpurun_out/r05_staged_sweep.jsonl
 H=tests/cpp/multipart_harness
 run() {  # case-name, args...
   local name=$1; shift
-  timeout -k 10 300 env QSMD5_BACKEND=auto $H --aligned --repeat=2 "$@" > gpurun_out/_one.json || return 1
+  timeout -k 10 300 env QSMD5_BACKEND=${BACKEND:-auto} $H --aligned --repeat=2 "$@" > gpurun_out/_one.json || return 1
   python3 - "$name" >> $OUT <<'PY'
 import json, sys
 r = json.load(open("gpurun_out/_one.json"))
@@ -30,6 +30,8 @@ for P in 128 512; do
   S=$((P * 10 * 1024 * 1024))
   run "waves_n5_P$P" --size=$S --pool=5 --pinned --no-pipeline || exit 1
   run "staged_n5_P$P" --size=$S --pool=5 --pinned --staged || exit 1
+  BACKEND=gpu run "staged_n5_gpu_P$P" --size=$S --pool=5 --pinned --staged || exit 1
+  BACKEND=cpu run "staged_n5_cpu_P$P" --size=$S --pool=5 --pinned --staged || exit 1
   run "staged_n5_pageable_pool_P$P" --size=$S --pool=5 --staged || exit 1
   for B in 64 1024; do
     run "staged_n5_staging${B}M_P$P" --size=$S --pool=5 --pinned --staged --staging=$((B << 20)) || exit 1
