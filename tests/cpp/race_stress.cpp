@@ -10,6 +10,7 @@
 //   - qsmd5_init (lazy, call_once) as their first call;
 //   - qsmd5_hash_one over pageable buffers (group commit merges these);
 //   - qsmd5_hash_batch / _ex over ragged, unaligned sub-ranges;
+//   - qsmd5_hash_read pulling ragged sub-ranges through a read callback;
 //   - the streaming context (MD5 class) fed in pieces;
 //   - qsmd5_alloc_pinned / qsmd5_free_pinned around a hash;
 //   - qsmd5_hex / qsmd5_base64;
@@ -114,7 +115,7 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
   }
   for (int r = 0; r < rounds; ++r) {
     uint8_t d[16];
-    switch ((t + r) % 5) {
+    switch ((t + r) % 6) {
       case 0: {  // one part, pageable, arbitrary offset and length
         const size_t off = next(s) % 61, len = next(s) % (max_len - 64) + 1;
         in_buf(buf, buf.data() + off, len, "hash_one");
@@ -216,6 +217,36 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
         else
           for (int i = 0; i < n; ++i)
             check((const uint8_t*)ch[i].ptr, ch[i].len, dg.data() + 16 * i, "split batch", t, r);
+        break;
+      }
+      case 5: {  // pull-driven batch (qsmd5_hash_read): the library reads sub-ranges in windows
+        struct Src {
+          const uint8_t* base;
+          std::vector<size_t> off;
+          std::vector<uint64_t> len;
+          static uint64_t read(void* user, size_t c, uint64_t o, uint64_t n, void* dst) {
+            const Src* s = static_cast<const Src*>(user);
+            if (o + n > s->len[c]) return 0;
+            memcpy(dst, s->base + s->off[c] + o, n);
+            return n;
+          }
+        } src;
+        src.base = buf.data();
+        const int n = 1 + (int)(next(s) % 24);
+        for (int i = 0; i < n; ++i) {
+          size_t len = next(s) % (max_len / 3 + 1);
+          const size_t off = next(s) % (buf.size() - std::min(len, buf.size()) + 1);
+          len = std::min(len, buf.size() - off);
+          in_buf(buf, buf.data() + off, len, "hash_read");
+          src.off.push_back(off);
+          src.len.push_back(len);
+        }
+        const uint64_t staging = (uint64_t)(64u << 10) << (next(s) % 7);  // 64 KiB .. 4 MiB
+        std::vector<uint8_t> dg(16 * n);
+        if ((rc = qsmd5_hash_read(src.len.data(), n, &Src::read, &src, staging, (uint8_t(*)[16])dg.data(), 0)) != 0)
+          fail("hash_read", rc, t, r);
+        else
+          for (int i = 0; i < n; ++i) check(buf.data() + src.off[i], src.len[i], dg.data() + 16 * i, "hash_read", t, r);
         break;
       }
     }
