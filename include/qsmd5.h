@@ -304,7 +304,8 @@ QSMD5_API int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t
  * run side by side, each with its own stream and staging, up to
  * QSMD5_READ_SLOTS per GPU at a time (default 4, at most 8; each slot holds
  * up to staging_bytes of pinned host memory (two regions) and staging_bytes / 2
- * of HBM, taken on first use); a further call waits for a slot.  One bound GPU
+ * of HBM, taken on first use and kept until qsmd5_shutdown); a further call
+ * waits for a slot.  One bound GPU
  * hashes a whole call: the one with the fewest such calls in flight (the
  * first on a tie), so with QSMD5_DEVICES binding several, files flushed at
  * once spread over the GPUs. */
