@@ -10,11 +10,17 @@
 //   3. hash all parts of all files in ONE qsmd5_hash_batch call instead of one
 //      md5(buffer) per part (QSClient.cpp:370, 446).
 //
-// usage: qsmd5sum [-b MiB] [--parts] [--threshold MiB] [--min-part MiB] FILE...
+// --read: instead of mapping the files, let the library pull each part's
+// bytes with pread(2) in column windows through its bounded pinned staging
+// (qsmd5_hash_read, the pull-driven batch): the same one batch over every
+// part, for files of any size, with at most --staging MiB staged at a time.
+//
+// usage: qsmd5sum [-b MiB] [--parts] [--threshold MiB] [--min-part MiB] [--read [--staging MiB]] FILE...
 //   default output: "<md5>  <file>" for files below the multipart threshold,
 //   and one line per part for larger files (or for every file with --parts):
 //   "<md5>  <file>#<part> <offset> <size>"
 // Exit status: 0 ok, 1 usage or I/O error, 2 GPU error.
+#include <errno.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -35,7 +41,43 @@ struct FileParts {
   uint64_t size = 0;
   std::vector<qsmd5_part> parts;
   const uint8_t* data = nullptr;  // the file, mapped read-only (nullptr when empty)
+  int fd = -1;                    // --read: kept open for pread
 };
+
+// --read: chunk c of the batch is part `part` of file `file`
+struct PartRef {
+  const FileParts* file;
+  uint64_t offset;
+};
+
+uint64_t pread_part(void* user, size_t chunk, uint64_t offset, uint64_t len, void* dst) {
+  const PartRef& r = (*static_cast<const std::vector<PartRef>*>(user))[chunk];
+  uint64_t done = 0;
+  while (done < len) {
+    const ssize_t got = pread(r.file->fd, static_cast<char*>(dst) + done, len - done,
+                              (off_t)(r.offset + offset + done));
+    if (got <= 0) break;  // a short count fails the batch with -EIO
+    done += (uint64_t)got;
+  }
+  return done;
+}
+
+bool open_file(const char* path, FileParts& f, std::string& err) {
+  f.fd = open(path, O_RDONLY);
+  if (f.fd < 0) {
+    err = std::string("cannot open ") + path;
+    return false;
+  }
+  struct stat st;
+  if (fstat(f.fd, &st) != 0) {
+    err = std::string("cannot stat ") + path;
+    return false;
+  }
+  f.path = path;
+  f.size = (uint64_t)st.st_size;
+  (void)posix_fadvise(f.fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+  return true;
+}
 
 bool read_file(const char* path, FileParts& f, std::string& err) {
   const int fd = open(path, O_RDONLY);
@@ -70,7 +112,8 @@ bool read_file(const char* path, FileParts& f, std::string& err) {
 
 int main(int argc, char** argv) {
   uint64_t buf_mib = 10, threshold_mib = 20, min_part_mib = 4;  // configure/Default.cpp:159-177
-  bool all_parts = false;
+  uint64_t staging_mib = 0;  // --staging (0: the library's default)
+  bool all_parts = false, pull = false;
   std::vector<const char*> files;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "-b") && i + 1 < argc) {
@@ -81,9 +124,13 @@ int main(int argc, char** argv) {
       min_part_mib = strtoull(argv[++i], nullptr, 10);
     } else if (!strcmp(argv[i], "--parts")) {
       all_parts = true;
+    } else if (!strcmp(argv[i], "--read")) {
+      pull = true;
+    } else if (!strcmp(argv[i], "--staging") && i + 1 < argc) {
+      staging_mib = strtoull(argv[++i], nullptr, 10);
     } else if (argv[i][0] == '-') {
-      fprintf(stderr, "usage: %s [-b MiB] [--parts] [--threshold MiB] [--min-part MiB] FILE...\n",
-              argv[0]);
+      fprintf(stderr, "usage: %s [-b MiB] [--parts] [--threshold MiB] [--min-part MiB] "
+              "[--read [--staging MiB]] FILE...\n", argv[0]);
       return 1;
     } else {
       files.push_back(argv[i]);
@@ -99,7 +146,7 @@ int main(int argc, char** argv) {
   int rc = 0;
   for (size_t k = 0; k < files.size() && rc == 0; ++k) {
     std::string err;
-    if (!read_file(files[k], fs[k], err)) {
+    if (!(pull ? open_file(files[k], fs[k], err) : read_file(files[k], fs[k], err))) {
       fprintf(stderr, "qsmd5sum: %s\n", err.c_str());
       rc = 1;
       break;
@@ -117,7 +164,21 @@ int main(int argc, char** argv) {
     for (const qsmd5_part& p : fs[k].parts) chunks.push_back({fs[k].data + p.offset, p.size});
   }
   std::vector<uint8_t> dig(16 * chunks.size());
-  if (rc == 0 && !chunks.empty()) {
+  if (rc == 0 && !chunks.empty() && pull) {
+    std::vector<uint64_t> lens;
+    std::vector<PartRef> refs;
+    for (const FileParts& f : fs)
+      for (const qsmd5_part& p : f.parts) {
+        lens.push_back(p.size);
+        refs.push_back({&f, p.offset});
+      }
+    int e = qsmd5_hash_read(lens.data(), lens.size(), &pread_part, &refs, staging_mib * MiB,
+                            reinterpret_cast<uint8_t(*)[16]>(dig.data()), 0);
+    if (e != 0) {
+      fprintf(stderr, "qsmd5sum: hashing failed: %s (%s)\n", qsmd5_strerror(e), qsmd5_last_error());
+      rc = e == -EIO ? 1 : 2;
+    }
+  } else if (rc == 0 && !chunks.empty()) {
     // the files were read into host memory: no per-part pointer query
     int e = qsmd5_hash_batch_ex(chunks.data(), chunks.size(),
                                 reinterpret_cast<uint8_t(*)[16]>(dig.data()), QSMD5_FLAG_HOST);
@@ -142,7 +203,9 @@ int main(int argc, char** argv) {
       }
     }
   }
-  for (FileParts& f : fs)
+  for (FileParts& f : fs) {
     if (f.data) munmap(const_cast<uint8_t*>(f.data), f.size);
+    if (f.fd >= 0) close(f.fd);
+  }
   return rc;
 }

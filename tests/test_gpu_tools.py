@@ -1,8 +1,9 @@
 """qsmd5sum: the batch caller end to end on the GPU.
 
-Files are sliced like QSTransferManager::PrepareUpload, gathered into pinned
-buffers and hashed in one qsmd5_hash_batch call; every printed digest is
-checked against the pinned oracle on the same byte range.
+Files are sliced like QSTransferManager::PrepareUpload and hashed in one
+call: mapped, through qsmd5_hash_batch, or pulled with pread through
+qsmd5_hash_read (--read); every printed digest is checked against the pinned
+oracle on the same byte range.
 """
 import os
 import subprocess
@@ -19,7 +20,11 @@ MiB = 1 << 20
 TOOL = os.path.join(ROOT, "qsfs-fuse_amd", "bin", "qsmd5sum")
 
 
-def test_qsmd5sum_parts_match_oracle():
+@pytest.mark.parametrize("mode", [[], ["--read"], ["--read", "--staging", "1"]],
+                         ids=["mapped", "pulled", "pulled_1MiB_staging"])
+def test_qsmd5sum_parts_match_oracle(mode):
+    """Mapped files in one qsmd5_hash_batch, or (--read, round 5) every part
+    pulled with pread through qsmd5_hash_read's bounded staging."""
     if not os.path.exists(TOOL):
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "qsfs-fuse_amd")])
     sizes = [0, 5, 19 * MiB, 20 * MiB, 21 * MiB + 3, 25 * MiB, 64 * MiB + 1]
@@ -32,7 +37,7 @@ def test_qsmd5sum_parts_match_oracle():
                 f.write(b)
             paths.append(p)
             blobs.append(b)
-        out = subprocess.run([TOOL] + paths, capture_output=True, text=True, timeout=300)
+        out = subprocess.run([TOOL] + mode + paths, capture_output=True, text=True, timeout=300)
         assert out.returncode == 0, out.stderr
         lines = out.stdout.strip().splitlines()
         want = []
@@ -47,7 +52,7 @@ def test_qsmd5sum_parts_match_oracle():
                         q.part_number, q.offset, q.size))
         assert lines == want
         # -b 1: 1 MiB parts (the -b option of qsfs, Parser.cpp:167)
-        out = subprocess.run([TOOL, "-b", "1", "--parts", paths[5]], capture_output=True,
+        out = subprocess.run([TOOL, "-b", "1", "--parts"] + mode + [paths[5]], capture_output=True,
                              text=True, timeout=300)
         assert out.returncode == 0, out.stderr
         assert len(out.stdout.strip().splitlines()) == 25
