@@ -18,10 +18,10 @@ with open(sys.argv[1], 'wb') as f:
 : > $O
 for mode in "" "--read"; do
   for pass in 1 2; do
-    t0=$(date +%s.%N)
+    t0=$(date +%s%N)
     timeout -k 10 120 qsfs-fuse_amd/bin/qsmd5sum $mode --parts "$F" > /tmp/qsmd5sum_out_$pass.txt || exit 1
-    t1=$(date +%s.%N)
-    echo "mode=${mode:-mapped} pass=$pass seconds=$(echo "$t1 - $t0" | bc) parts=$(wc -l < /tmp/qsmd5sum_out_$pass.txt) digest_of_output=$(md5sum < /tmp/qsmd5sum_out_$pass.txt | cut -c1-32)" >> $O
+    t1=$(date +%s%N)
+    echo "mode=${mode:-mapped} pass=$pass seconds=$(( (t1 - t0) / 1000000 ))e-3 parts=$(wc -l < /tmp/qsmd5sum_out_$pass.txt) digest_of_output=$(md5sum < /tmp/qsmd5sum_out_$pass.txt | cut -c1-32)" >> $O
   done
 done
 rm -f "$F"
