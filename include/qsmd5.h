@@ -98,6 +98,12 @@ typedef struct qsmd5_part {
 #define QSMD5_FLAG_ALIGNED16 2      /* device_async_ex: caller promises 16-B-aligned chunk ptrs */
 #define QSMD5_FLAG_GPU_ONLY 8       /* hash_batch_ex: gfx950 kernels only, no CPU routing/fallback */
 #define QSMD5_FLAG_CPU_ONLY 16      /* hash_batch_ex: the library's CPU MD5 only */
+#define QSMD5_FLAG_BACKGROUND 32    /* hash_batch_ex / hash_read / route: the caller hides this
+                                     * batch's latency behind other work (a pre-hash running ahead
+                                     * of the uploads): under QSMD5_BACKEND=auto it goes to the GPU
+                                     * whenever one is usable, leaving the host's cores to the
+                                     * daemon (a GPU failure still falls back to the CPU); without
+                                     * a usable GPU, routed as usual. */
 #define QSMD5_FLAG_HOST 4           /* hash_batch_ex: caller promises every chunk is host memory
                                      * (pageable, pinned or registered), as qsfs's part buffers
                                      * are; skips pointer classification (otherwise one query per

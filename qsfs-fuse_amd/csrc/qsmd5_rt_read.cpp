@@ -460,15 +460,16 @@ int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* u
     return rc;
   };
   if (b == kCpu) return on_cpu("forced");
-  if (b == kAuto) {
-    if (g_gpu_lost.load()) return on_cpu("gpu-lost");
+  const bool background = b == kAuto && (flags & QSMD5_FLAG_BACKGROUND) && qsmd5_device_count() > 0;
+  if (b == kAuto && g_gpu_lost.load()) return on_cpu("gpu-lost");
+  if (b == kAuto && !background) {
     // price the hashing as for a batch of host chunks of these lengths
     const double read_ms = 1e3 * (double)J.total / kGiB / read_gibs();
     if (std::max(read_ms, cpu_read_model_ms() / cpu_efficiency()) <
         std::max(read_ms, gpu_est_ms(longest, J.total)))
       return on_cpu("size");
   }
-  log_read("gpu", b == kGpu ? "forced" : "size", J);
+  log_read("gpu", b == kGpu ? "forced" : background ? "background" : "size", J);
   int rc = ensure_init();
   bool sticky = false;
   if (rc == 0) {

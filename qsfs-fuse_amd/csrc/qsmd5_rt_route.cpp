@@ -904,13 +904,15 @@ int hash_routed(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
     return rc;
   };
   if (b == kCpu) return on_cpu("forced");
-  if (b == kAuto) {
+  const bool background = b == kAuto && (gflags & QSMD5_FLAG_BACKGROUND) && qsmd5_device_count() > 0;
+  if (b == kAuto && !background) {
     if (g_gpu_lost.load()) return on_cpu("gpu-lost");
     if (cpu_is_faster(chunks, n, gflags)) return on_cpu("size");
     const std::vector<uint32_t> to_cpu = plan_split(chunks, n, gflags);
     if (!to_cpu.empty()) return run_split(chunks, n, digests, gflags, to_cpu);
   }
-  log_call("gpu", b == kGpu ? "forced" : "size", n, chunks);
+  if (background && g_gpu_lost.load()) return on_cpu("gpu-lost");
+  log_call("gpu", b == kGpu ? "forced" : background ? "background" : "size", n, chunks);
   bool sticky = false;
   int rc = gpu_attempt(chunks, n, digests, gflags, &sticky);
   if (rc == 0) {

@@ -414,6 +414,8 @@ int qsmd5_last_backend(void) { return t_last_backend; }
 int qsmd5_route(const qsmd5_chunk* chunks, size_t n, int flags) {
   if (n && !chunks) return fail(-EINVAL, "qsmd5: NULL chunks");
   return guarded([&] {
+    if ((flags & QSMD5_FLAG_BACKGROUND) && qsmd5_device_count() > 0 && !g_gpu_lost.load())
+      return QSMD5_BACKEND_GPU;  // latency hidden: the cores stay the daemon's
     if (cpu_is_faster(chunks, n, flags)) return QSMD5_BACKEND_CPU;
     return plan_split(chunks, n, flags).empty() ? QSMD5_BACKEND_GPU : QSMD5_BACKEND_SPLIT;
   });

@@ -416,6 +416,12 @@ struct StagedOptions {
   // CPU's, ~ms) instead of a GPU wave's chain time (~85 ms per 10 MiB part),
   // and each larger wave is pre-hashed while the smaller one before it uploads.
   size_t first_wave_parts = 0;
+  // With pipeline: the waves after the first are pre-hashed while the one
+  // before them uploads, so their latency is hidden; they go out with
+  // QSMD5_FLAG_BACKGROUND (the GPU whenever one is usable, leaving the host's
+  // cores to the daemon's own threads).  The first wave, which the first
+  // upload waits for, is routed for speed.  false: every wave for speed.
+  bool background_waves = true;
   bool pipeline = true;        // pre-hash the next wave on a helper thread while this one uploads
                                // (read_range then runs there too: PrehashOptions::pipeline)
   bool upload_releases = false;  // as PrehashOptions::upload_releases
@@ -464,7 +470,7 @@ struct StagedWave {
 
 template <class ReadRange>
 StagedWave prehash_wave(const std::vector<qsmd5_part>& parts, size_t first, size_t count,
-                        ReadRange& read_range, const StagedOptions& opt) {
+                        ReadRange& read_range, const StagedOptions& opt, int extra_flags = 0) {
   StagedWave w;
   w.first = first;
   if (opt.should_continue && !opt.should_continue()) {
@@ -478,7 +484,7 @@ StagedWave prehash_wave(const std::vector<qsmd5_part>& parts, size_t first, size
   w.dig.resize(16 * count);
   RangeReader<ReadRange> rr{&parts, first, &read_range, nullptr};
   const int rc = qsmd5_hash_read(lens.data(), count, &RangeReader<ReadRange>::thunk, &rr, opt.staging_bytes,
-                                 reinterpret_cast<uint8_t(*)[16]>(w.dig.data()), opt.flags);
+                                 reinterpret_cast<uint8_t(*)[16]>(w.dig.data()), opt.flags | extra_flags);
   if (rr.err) std::rethrow_exception(rr.err);
   check(rc, "qsmd5_hash_read");
   w.backend = qsmd5_last_backend();  // this thread's call
@@ -529,7 +535,9 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
     return prev ? std::min(per, 2 * prev) : std::min(per, opt.first_wave_parts);
   };
   auto prep = [&](size_t first, size_t count) {
-    return detail::prehash_wave(parts, first, std::min(count, parts.size() - first), read_range, opt);
+    // a wave pre-hashed behind an upload (not the first) may take its time
+    const int extra = (first > 0 && opt.pipeline && opt.background_waves) ? QSMD5_FLAG_BACKGROUND : 0;
+    return detail::prehash_wave(parts, first, std::min(count, parts.size() - first), read_range, opt, extra);
   };
   std::future<detail::StagedWave> ahead;
   auto drain_ahead = [&]() noexcept {

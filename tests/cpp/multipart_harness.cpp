@@ -315,6 +315,7 @@ int main(int argc, char** argv) {
   uint64_t size = 64ull * 10 * 1024 * 1024;
   size_t pool_n = 5, files = 1, naive_wave = 0, max_wave = 0;
   bool aligned = false, pinned = false, slab = false, reg = false, pipeline = true, staged = false;
+  bool foreground = false;  // --foreground: StagedOptions::background_waves = false
   uint64_t staging = 0;
   size_t wave_parts = 0, first_wave = 0;
   size_t cpus = 0, load_threads = 0;  // --cpus: the process's cores; --load: spinning threads on them
@@ -349,6 +350,7 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--cpus=")) cpus = strtoull(v, nullptr, 0);
     else if (const char* v = val("--load=")) load_threads = strtoull(v, nullptr, 0);
     else if (a == "--staged") staged = true;
+    else if (a == "--foreground") foreground = true;
     else if (a == "--aligned") aligned = true;
     else if (a == "--pinned") pinned = true;
     else if (a == "--slab") slab = true;
@@ -540,6 +542,7 @@ int main(int argc, char** argv) {
               so.staging_bytes = staging;
               so.wave_parts = wave_parts;
               so.first_wave_parts = first_wave;
+              so.background_waves = !foreground;
               so.pipeline = pipeline;
               so.upload_releases = opt.upload_releases;
               so.should_continue = opt.should_continue;
@@ -601,6 +604,7 @@ int main(int argc, char** argv) {
     sum.gpu_waves += s.gpu_waves;
     sum.cpu_waves += s.cpu_waves;
     sum.split_waves += s.split_waves;
+    sum.rehashed += s.rehashed;
     sum.widest_wave = std::max(sum.widest_wave, s.widest_wave);
     sum.gather_s += s.gather_s;
     sum.hash_s += s.hash_s;
@@ -627,8 +631,9 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < hash_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", hash_runs[i]);
   printf("], \"wall_s_runs\": [");
   for (size_t i = 0; i < wall_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", wall_runs[i]);
-  printf("], \"cpus\": %zu, \"load_threads\": %zu, \"cpu_efficiency\": %.4f, \"wave_parts\": %zu, \"first_wave\": %zu",
-         cpus, load_threads, cpu_eff, wave_parts, first_wave);
+  printf("], \"cpus\": %zu, \"load_threads\": %zu, \"cpu_efficiency\": %.4f, \"wave_parts\": %zu, \"first_wave\": %zu, "
+         "\"background_waves\": %s, \"rehashed\": %zu",
+         cpus, load_threads, cpu_eff, wave_parts, first_wave, foreground ? "false" : "true", sum.rehashed);
   printf(", \"busy_threads\": {%s}, \"cpu_s_runs\": [", busy_threads().c_str());
   for (size_t i = 0; i < cpu_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", cpu_runs[i]);
   printf("], \"md5\": %s, \"md5_files\": [", md5_list(md5[0]).c_str());

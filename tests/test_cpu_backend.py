@@ -494,3 +494,16 @@ def test_shutdown_not_starved_by_overlapping_calls(tmp_path):
     import json
     r = json.loads(out.stdout.strip().splitlines()[-1])
     assert not r["starved"] and r["shutdown_s"] < 5.0 and r["calls_after"] > 0
+
+
+def test_background_flag_without_a_gpu_routes_as_usual(monkeypatch):
+    """QSMD5_FLAG_BACKGROUND (round 5): a batch whose latency the caller
+    hides goes to the GPU whenever one is usable; without one it is routed
+    as any batch (a lone part to the CPU), and hashes right."""
+    if qsmd5.device_count() > 0:
+        pytest.skip("GPU present (tests/test_gpu_routing.py covers the GPU side)")
+    monkeypatch.setenv("QSMD5_BACKEND", "auto")
+    data = lcg_bytes(31, 3 * MiB)
+    assert qsmd5.route([3 * MiB], flags=qsmd5.FLAG_BACKGROUND) == qsmd5.BACKEND_CPU
+    got = qsmd5.hash_batch([(ctypes.addressof(data), 3 * MiB)], flags=qsmd5.FLAG_BACKGROUND)
+    assert got == md5_many([(data, 3 * MiB)])

@@ -307,3 +307,27 @@ def test_device_chunks_pay_their_read_back_in_routing(auto):
     gold = json.load(open(os.path.join(ROOT, "tests", "golden", "batch_10MiB.json")))["md5"]
     assert [d.hex() for d in got] == gold[:n]
     print("n=%d device 10 MiB chunks: GPU; as host memory: CPU; rates %s" % (n, r))
+
+
+def test_background_batches_take_the_gpu(auto):
+    """QSMD5_FLAG_BACKGROUND (round 5): a lone part, and a pull-driven batch of
+    8 parts -- both the CPU's on speed -- go to the GPU when the caller says
+    their latency is hidden (the staged pre-hash's later waves), with the
+    oracle's digests; without the flag they stay on the CPU."""
+    MiB = 1 << 20
+    data = lcg_bytes(41, 8 * MiB)
+    one = [(ctypes.addressof(data), 8 * MiB)]
+    assert qsmd5.route([8 * MiB]) == qsmd5.BACKEND_CPU
+    assert qsmd5.route([8 * MiB], flags=qsmd5.FLAG_BACKGROUND) == qsmd5.BACKEND_GPU
+    want = md5_many(one)
+    assert qsmd5.hash_batch(one, flags=qsmd5.FLAG_BACKGROUND) == want
+    assert qsmd5.last_backend() == qsmd5.BACKEND_GPU
+    assert qsmd5.hash_batch(one) == want and qsmd5.last_backend() == qsmd5.BACKEND_CPU
+    lens = [MiB] * 8
+
+    def read(chunk, off, n, dst):
+        ctypes.memmove(dst, ctypes.addressof(data) + chunk * MiB + off, n)
+        return n
+    want8 = md5_many([(ctypes.addressof(data) + i * MiB, MiB) for i in range(8)])
+    assert qsmd5.hash_read(lens, read, flags=qsmd5.FLAG_BACKGROUND) == want8
+    assert qsmd5.last_backend() == qsmd5.BACKEND_GPU
