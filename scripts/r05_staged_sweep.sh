@@ -39,6 +39,7 @@ for P in 128 512; do
   run "staged_n5_waves64_P$P" --size=$S --pool=5 --pinned --staged --wave-parts=64 || exit 1
   run "staged_n5_upload10ms_P$P" --size=$S --pool=5 --pinned --staged --wave-parts=64 --upload-ms=10 || exit 1
   run "staged_n5_ramp4_upload10ms_P$P" --size=$S --pool=5 --pinned --staged --wave-parts=64 --first-wave=4 --upload-ms=10 || exit 1
+  run "staged_n5_ramp4_upload10ms_fg_P$P" --size=$S --pool=5 --pinned --staged --wave-parts=64 --first-wave=4 --upload-ms=10 --foreground || exit 1
   run "staged_n5_whole_upload10ms_P$P" --size=$S --pool=5 --pinned --staged --upload-ms=10 || exit 1
   run "waves_n5_upload10ms_P$P" --size=$S --pool=5 --pinned --upload-ms=10 || exit 1
 done
