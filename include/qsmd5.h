@@ -104,6 +104,10 @@ typedef struct qsmd5_part {
                                      * whenever one is usable, leaving the host's cores to the
                                      * daemon (a GPU failure still falls back to the CPU); without
                                      * a usable GPU, routed as usual. */
+#define QSMD5_FLAG_READ_PARALLEL 64 /* hash_read: `read` may run on several library threads at
+                                     * once, for different chunks of a window (pread on a file,
+                                     * say): QSMD5_READ_THREADS of them (default 4, at most 16).
+                                     * Without it, read runs on the calling thread only. */
 #define QSMD5_FLAG_HOST 4           /* hash_batch_ex: caller promises every chunk is host memory
                                      * (pageable, pinned or registered), as qsfs's part buffers
                                      * are; skips pointer classification (otherwise one query per
@@ -300,8 +304,10 @@ QSMD5_API int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t
  * *   call with -EIO (the reference stops the upload on a short read,
  *   QSTransferManager.cpp:625-643); nothing is hashed from it.
  *
- * read runs on the calling thread only, one window at a time, with each
- * chunk's windows in increasing offset order and every byte asked for once --
+ * read runs on the calling thread only (QSMD5_FLAG_READ_PARALLEL: on several
+ * threads at once, each chunk's windows still in order), one window at a
+ * time, with each chunk's windows in increasing offset order and every byte
+ * asked for once --
  * except that in QSMD5_BACKEND=auto a GPU failure re-runs the whole batch on
  * the CPU, asking for every byte again from offset 0.  It may call other qsmd5
  * entry points (not qsmd5_shutdown).  lens[i] < 2^38.  Routed like

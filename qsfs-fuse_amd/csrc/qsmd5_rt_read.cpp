@@ -41,24 +41,58 @@ struct ReadJob {
   uint64_t total = 0;
   bool short_read = false;       // the caller's read came back short: not a GPU failure
   double read_s = 0;             // time in the caller's reads (the read-rate estimate)
+  size_t readers = 1;            // threads calling read at once (QSMD5_FLAG_READ_PARALLEL)
 };
 
 // The window of column j of group g for its `active` live lanes, lane k at
 // dst + k * stride.  A count other than asked fails the job (-EIO), as a short
 // ReadNoLoad stops the reference's upload (QSTransferManager.cpp:625-643).
+// With QSMD5_FLAG_READ_PARALLEL the window's rows are read by J.readers
+// threads at once (row k on thread k % readers); the first short read stops
+// them all and is reported from this thread (fail() keeps its message per
+// thread).
 int fill_window(ReadJob& J, const ReadGroup& g, uint32_t j, size_t active, uint8_t* dst) {
   const uint64_t off = (uint64_t)j * g.W;
-  for (size_t k = 0; k < active; ++k) {
-    const uint32_t c = J.order[g.first + k];
-    const uint64_t w = ReadPlan::col_bytes(g, J.len[c], j);
-    if (!w) continue;
-    const uint64_t got = J.read(J.user, c, off, w, dst + k * g.stride);
-    if (got != w) {
-      J.short_read = true;
-      return fail(-EIO, "qsmd5_hash_read: short read of chunk " + std::to_string(c) + " at offset " +
-                            std::to_string(off) + ": " + std::to_string(got) + " of " +
-                            std::to_string(w) + " bytes");
+  struct Short {
+    std::atomic<bool> hit{false};
+    std::mutex mu;
+    uint32_t c = 0;
+    uint64_t got = 0, want = 0;
+  } bad;
+  auto rows = [&](size_t first, size_t step) noexcept {
+    for (size_t k = first; k < active && !bad.hit.load(std::memory_order_relaxed); k += step) {
+      const uint32_t c = J.order[g.first + k];
+      const uint64_t w = ReadPlan::col_bytes(g, J.len[c], j);
+      if (!w) continue;
+      const uint64_t got = J.read(J.user, c, off, w, dst + k * g.stride);
+      if (got != w) {
+        std::lock_guard<std::mutex> lk(bad.mu);
+        if (!bad.hit.load()) {
+          bad.c = c;
+          bad.got = got;
+          bad.want = w;
+          bad.hit.store(true);
+        }
+        return;
+      }
     }
+  };
+  const size_t T = std::min(J.readers, std::max<size_t>(active, 1));
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < T; ++t) {
+    try {
+      th.emplace_back(rows, t, T);
+    } catch (...) {  // no thread: this one reads that share too
+      rows(t, T);
+    }
+  }
+  rows(0, T);
+  for (auto& t : th) t.join();
+  if (bad.hit.load()) {
+    J.short_read = true;
+    return fail(-EIO, "qsmd5_hash_read: short read of chunk " + std::to_string(bad.c) + " at offset " +
+                          std::to_string(off) + ": " + std::to_string(bad.got) + " of " +
+                          std::to_string(bad.want) + " bytes");
   }
   return 0;
 }
@@ -237,7 +271,8 @@ bool read_lanes(size_t act, size_t T) {
 
 // The CPU backend of a pull-driven batch: the same windows, double-buffered
 // like the GPU's: the calling thread reads window s + 1 (the caller's reads
-// stay on its thread) while worker threads fold window s's rows into their
+// stay on its thread, or its reader threads with QSMD5_FLAG_READ_PARALLEL)
+// while worker threads fold window s's rows into their
 // chunks' running contexts (md5_cpu.h Ctx) -- 16 rows at a time per thread in
 // the AVX-512 lanes where read_lanes says so (the rows' whole blocks continue
 // their chunks' states; a final column's last len % 64 bytes go through the
@@ -422,6 +457,8 @@ int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* u
   ReadJob J;
   J.read = read;
   J.user = user;
+  if (flags & QSMD5_FLAG_READ_PARALLEL)
+    J.readers = (size_t)std::min<uint64_t>(16, std::max<uint64_t>(1, env_u64("QSMD5_READ_THREADS", 4)));
   J.len.resize(n);
   uint64_t longest = 0;
   for (size_t i = 0; i < n; ++i) {

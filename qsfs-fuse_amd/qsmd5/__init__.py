@@ -23,7 +23,7 @@ __all__ = [
     "Md5Error", "lib", "lib_path", "shutdown", "hexdigest", "md5", "md5_stream", "MD5", "hash_batch",
     "hash_one", "hash_device", "hash_parts", "plan_parts", "kernel_choice", "device_count",
     "alloc_pinned", "free_pinned", "hash_read", "buffer_reader", "register_host", "unregister_host", "synth_fill_lcg", "last_timing", "Part", "etag_matches",
-    "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST", "FLAG_GPU_ONLY", "FLAG_BACKGROUND",
+    "verify_etag", "FLAG_REF_TRUNCATE32", "FLAG_ALIGNED16", "FLAG_HOST", "FLAG_GPU_ONLY", "FLAG_BACKGROUND", "FLAG_READ_PARALLEL",
     "FLAG_CPU_ONLY", "stats", "rates", "cpu_efficiency", "last_backend", "route", "BACKEND_GPU", "BACKEND_CPU", "BACKEND_SPLIT",
 ]
 
@@ -216,6 +216,7 @@ FLAG_HOST = 4  # every chunk is host memory: skip the per-chunk pointer query
 FLAG_GPU_ONLY = 8  # gfx950 kernels only: no CPU routing or fallback
 FLAG_CPU_ONLY = 16  # the library's CPU MD5 only
 FLAG_BACKGROUND = 32  # latency hidden by the caller: the GPU whenever one is usable (auto)
+FLAG_READ_PARALLEL = 64  # hash_read: read may run on several library threads at once
 BACKEND_GPU = 1
 BACKEND_CPU = 2
 BACKEND_SPLIT = 3  # both at once: the longest host chunks on the CPU, the rest on the GPU

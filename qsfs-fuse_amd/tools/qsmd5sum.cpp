@@ -172,8 +172,9 @@ int main(int argc, char** argv) {
         lens.push_back(p.size);
         refs.push_back({&f, p.offset});
       }
+    // pread is thread-safe: let the library read a window's parts on several threads
     int e = qsmd5_hash_read(lens.data(), lens.size(), &pread_part, &refs, staging_mib * MiB,
-                            reinterpret_cast<uint8_t(*)[16]>(dig.data()), 0);
+                            reinterpret_cast<uint8_t(*)[16]>(dig.data()), QSMD5_FLAG_READ_PARALLEL);
     if (e != 0) {
       fprintf(stderr, "qsmd5sum: hashing failed: %s (%s)\n", qsmd5_strerror(e), qsmd5_last_error());
       rc = e == -EIO ? 1 : 2;

@@ -269,3 +269,16 @@ def test_concurrent_reads_contend_for_slots():
     for job in jobs:
         assert job["got"] == md5_many(job["chunks"])
         job["rd"].check_contract()
+
+
+def test_read_parallel_flag_on_the_gpu(golden, monkeypatch):
+    """QSMD5_FLAG_READ_PARALLEL on the GPU path: 512 x 10 MiB parts read by 4
+    library threads per window, every digest golden, the read contract kept."""
+    monkeypatch.setenv("QSMD5_READ_THREADS", "4")
+    gold = golden("batch_10MiB.json")["md5"][:512]
+    L = 10 * MiB
+    host = _host_lcg(512, L, 12345)
+    rd = Reader([(host.ctypes.data + i * L, L) for i in range(512)])
+    got = qsmd5.hash_read([L] * 512, rd, flags=GPU | qsmd5.FLAG_READ_PARALLEL)
+    assert [d.hex() for d in got] == gold
+    rd.check_contract()

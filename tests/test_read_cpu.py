@@ -192,3 +192,26 @@ def test_read_routing_compares_wall_times(monkeypatch):
             assert any(want in l and "(read)" in l for l in lines), (gibs, lines)
     finally:
         qsmd5.set_log_callback(None)
+
+
+@pytest.mark.parametrize("readers", ["1", "3", "8"])
+def test_read_parallel_flag(monkeypatch, readers):
+    """QSMD5_FLAG_READ_PARALLEL (round 5): the library may call read from
+    QSMD5_READ_THREADS threads at once, for different chunks of a window.
+    Same digests, every chunk's windows still in order and every byte read
+    once; a short read on any thread still fails the call with -EIO."""
+    monkeypatch.setenv("QSMD5_READ_THREADS", readers)
+    rng = random.Random(int(readers))
+    lens = [rng.choice([0, 1, 64, 65, 4096, 1 << 20, 3 * MiB + 7]) for _ in range(40)]
+    bufs = [lcg_bytes(900 + i, L) for i, L in enumerate(lens)]
+    rec = Recorder(bufs, lens)
+    got = qsmd5.hash_read(lens, rec, staging_bytes=1 << 20, flags=CPU | qsmd5.FLAG_READ_PARALLEL)
+    assert got == md5_many([(b, L) for b, L in zip(bufs, lens)])
+    rec.check_contract()
+    bad = Recorder(bufs, lens)
+    bad.lens = list(lens)
+    bad.lens[lens.index(3 * MiB + 7)] = MiB  # the reader says this chunk ends early
+    with pytest.raises(qsmd5.Md5Error) as e:
+        qsmd5.hash_read(lens, bad, staging_bytes=1 << 20, flags=CPU | qsmd5.FLAG_READ_PARALLEL)
+    assert e.value.code == -5  # -EIO
+    assert "short read of chunk %d" % lens.index(3 * MiB + 7) in str(e.value)
