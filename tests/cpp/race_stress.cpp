@@ -243,7 +243,9 @@ void worker(int t, int rounds, size_t max_len, std::atomic<int>* ready, int nthr
         }
         const uint64_t staging = (uint64_t)(64u << 10) << (next(s) % 7);  // 64 KiB .. 4 MiB
         std::vector<uint8_t> dg(16 * n);
-        if ((rc = qsmd5_hash_read(src.len.data(), n, &Src::read, &src, staging, (uint8_t(*)[16])dg.data(), 0)) != 0)
+        const int rflags = (r & 2) ? QSMD5_FLAG_READ_PARALLEL : 0;  // Src::read is thread-safe
+        if ((rc = qsmd5_hash_read(src.len.data(), n, &Src::read, &src, staging, (uint8_t(*)[16])dg.data(),
+                                  rflags)) != 0)
           fail("hash_read", rc, t, r);
         else
           for (int i = 0; i < n; ++i) check(buf.data() + src.off[i], src.len[i], dg.data() + 16 * i, "hash_read", t, r);
