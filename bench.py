@@ -194,6 +194,29 @@ def _traffic_from_profiles():
     return found
 
 
+def _clock_evidence():
+    """The headline kernel's effective clock from the newest committed clock
+    log (profiles/<round>_effective_clock.log: GRBM_GUI_ACTIVE / 8 XCDs / wall
+    per dispatch, scripts/summarize_clock.py), with the file it came from.
+    Read from the committed profile, not measured in this run."""
+    import re
+    pdir = os.path.join(ROOT, "profiles")
+    logs = sorted(f for f in os.listdir(pdir) if f.endswith("effective_clock.log")) if os.path.isdir(pdir) else []
+    for f in reversed(logs):
+        ghz = []
+        for line in open(os.path.join(pdir, f)):
+            if line.strip() == "" and ghz:
+                break  # the headline section is the first one
+            m = re.search(r"qsmd5_batch_pc64_kernel\s.*->\s*([0-9.]+) GHz", line)
+            if m:
+                ghz.append(float(m.group(1)))
+        if ghz:
+            return ("the kernel ran at %.3f-%.3f GHz over %d dispatches of this workload: GRBM_GUI_ACTIVE / "
+                    "8 XCDs / wall (profiles/%s, a committed PMC pass, not this run), so the 2.4 GHz cycle "
+                    "count above is the kernel's own" % (min(ghz), max(ghz), len(ghz), f))
+    return "not measured (no profiles/*_effective_clock.log)"
+
+
 def _host_mem_available():
     """Bytes of host memory this node can still give (MemAvailable, capped by
     the cgroup limit), or None."""
@@ -512,9 +535,7 @@ def main():
                       "cycles_per_64B_block_at_2p4GHz": round(kavg_ms * 1e-3 * 2.4e9 / (L / 64), 1),
                       "note": "MD5 is a serial chain per chunk; at batch=512 the job rate is "
                               "512 x the per-chain rate (SURVEY.md §0 item 5)",
-                      "clock_evidence": "the kernel runs at 2.398-2.400 GHz: GRBM_GUI_ACTIVE / 8 XCDs / "
-                                        "wall over its dispatches (profiles/r04_effective_clock.log), so "
-                                        "the 2.4 GHz cycle count above is the kernel's own"},
+                      "clock_evidence": _clock_evidence()},
         "parity": "ok: %d/%d digests == reference golden" % (ntot, ntot) if parity_ok else "FAIL",
         "process_group": pg,
         "cpu_baseline": None,

@@ -183,11 +183,23 @@ struct EventSet {
 // by side.  The stream and events are made on first use, the buffers grow
 // with the jobs (HostPinned / DevBuf reserve).
 constexpr int kMaxReadSlots = 8;
+constexpr int kMaxReadRegions = 4;  // staging regions per job (QSMD5_READ_REGIONS, default 2)
 struct ReadSlot {
-  hipStream_t stream = nullptr;
-  hipEvent_t copied[2] = {};  // the last H2D copy out of host region k
+  hipStream_t stream = nullptr;  // kernels (and, with QSMD5_READ_OVERLAP=0, the copies too)
+  hipStream_t copy = nullptr;    // window copies into the device regions
+  hipEvent_t copied[kMaxReadRegions] = {};  // the last H2D copy out of host region k (into device region k)
+  hipEvent_t hashed[kMaxReadRegions] = {};  // the last column kernel over device region k
   hipEvent_t done = nullptr;
-  HostPinned h_read, h_meta;  // two staging regions; descriptors + orders, then digests
+  // every event above, for creation and release
+  std::vector<hipEvent_t*> events() {
+    std::vector<hipEvent_t*> v = {&done};
+    for (int k = 0; k < kMaxReadRegions; ++k) {
+      v.push_back(&copied[k]);
+      v.push_back(&hashed[k]);
+    }
+    return v;
+  }
+  HostPinned h_read, h_meta;  // the staging regions; descriptors + orders, then digests
   DevBuf d_read, d_meta, d_state, d_dig;
 };
 
@@ -469,6 +481,8 @@ int run_sharded(const qsmd5_chunk* chunks, size_t n, uint8_t (*digests)[16], int
 
 // ---- pull-driven batches (qsmd5_rt_read.cpp) -------------------------------------
 constexpr uint64_t kDefaultReadStaging = 256ull << 20;  // QSMD5_READ_STAGING_BYTES
+void prewarm_read_slot(Dev& d);  // read slot 0's buffers at init (QSMD5_READ_PREWARM)
+void release_read_cache();       // the CPU path's cached staging (qsmd5_shutdown)
 int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* user,
                      uint64_t staging_bytes, uint8_t (*digests)[16], int flags);
 

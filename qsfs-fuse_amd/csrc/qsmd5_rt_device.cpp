@@ -165,12 +165,13 @@ int release_dev(Dev& d) {
       s = nullptr;
     }
   for (ReadSlot& rs : d.read_slot) {
-    if (rs.stream) {
-      chk(hipStreamSynchronize(rs.stream));
-      chk(hipStreamDestroy(rs.stream));
-      rs.stream = nullptr;
-    }
-    for (hipEvent_t* e : {&rs.copied[0], &rs.copied[1], &rs.done})
+    for (hipStream_t* s : {&rs.stream, &rs.copy})
+      if (*s) {
+        chk(hipStreamSynchronize(*s));
+        chk(hipStreamDestroy(*s));
+        *s = nullptr;
+      }
+    for (hipEvent_t* e : rs.events())
       if (*e) {
         chk(hipEventDestroy(*e));
         *e = nullptr;
@@ -233,6 +234,7 @@ static void do_init() {
   }
   r.shard_bytes = env_u64("QSMD5_SHARD_BYTES", 4ull << 30);
   (void)hipSetDevice(r.devs[0]->device);
+  prewarm_read_slot(*r.devs[0]);
   r.ready = true;
   r.init_rc = 0;
   if (log_wanted(QSMD5_LOG_INFO))

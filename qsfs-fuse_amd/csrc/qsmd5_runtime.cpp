@@ -98,6 +98,7 @@ int qsmd5_shutdown(void) {
     }
     g_gpu_chain_bits.store(0, std::memory_order_relaxed);  // a re-init times its GPU afresh
     r.devs.clear();
+    release_read_cache();
     {
       Registry& R = registry();
       std::lock_guard<std::mutex> rl(R.mu);

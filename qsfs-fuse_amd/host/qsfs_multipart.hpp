@@ -51,6 +51,7 @@
 #define QSFS_AMD_QSFS_MULTIPART_HPP_
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <condition_variable>
@@ -61,6 +62,9 @@
 #include <stdexcept>
 #include <string>
 #include <system_error>
+#include <thread>
+#include <type_traits>
+#include <utility>
 #include <vector>
 
 #include "qsfs_md5.hpp"
@@ -183,6 +187,12 @@ struct WaveStats {
   size_t widest_wave = 0;
   size_t rehashed = 0;   // upload_parts_staged: parts re-hashed from their buffer (source_changed)
   double gather_s = 0, hash_s = 0, upload_s = 0, wait_s = 0, wall_s = 0;
+  // upload_parts_staged's upload loop, on the calling thread (VERDICT r05 item
+  // 3): blocked in the pool's acquire(); in the loop's own read of a part into
+  // its buffer, or waiting for that part's read-ahead; inside upload().
+  // read_ahead = parts whose read ran behind the previous part's upload.
+  double acquire_s = 0, loop_read_s = 0, upload_call_s = 0;
+  size_t read_ahead = 0;
 };
 
 struct PrehashOptions {
@@ -425,8 +435,21 @@ struct StagedOptions {
   bool pipeline = true;        // pre-hash the next wave on a helper thread while this one uploads
                                // (read_range then runs there too: PrehashOptions::pipeline)
   bool upload_releases = false;  // as PrehashOptions::upload_releases
-  int flags = 0;               // qsmd5_hash_read flags (QSMD5_FLAG_GPU_ONLY / _CPU_ONLY)
+  int flags = 0;               // qsmd5_hash_read flags (QSMD5_FLAG_GPU_ONLY / _CPU_ONLY; with
+                               // QSMD5_FLAG_READ_PARALLEL read_range runs on several library
+                               // threads at once and must be thread-safe, as pread is)
   std::function<bool()> should_continue;  // as PrehashOptions::should_continue (thread-safe)
+  // With pipeline: while a part uploads, the next part of the wave is read
+  // into a buffer the pool has free at that moment (try_acquire, never a
+  // blocking acquire while this thread holds a buffer) on a helper thread, so
+  // the loop's own ReadNoLoad runs behind the upload instead of between
+  // uploads (512 reads of ~0.8 ms each, serial with the
+  // uploads, were the staged flow's 0.42 s over pure upload time).  The file
+  // then has two parts in flight for one flush, as the reference's async
+  // path has up to -n (QSTransferManager.cpp:654-659).  Needs a pool with
+  // try_acquire (without one the loop reads as the reference's does).  false:
+  // one buffer at a time, exactly the reference's loop.
+  bool read_ahead = true;
   // The pre-hash reads the file before the upload loop reads each part again
   // into its buffer: a write in between would send a Content-MD5 that does not
   // match the part (the reference hashes the very buffer it sends,
@@ -441,23 +464,131 @@ struct StagedOptions {
 namespace detail {
 
 // read_range(file_offset, len, char* dst) -> bytes copied (File::ReadNoLoad(...).first).
+// With QSMD5_FLAG_READ_PARALLEL in the flags, thunk runs on several library
+// threads at once: the first exception is kept (under a mutex)
+// and every later read returns 0 at once.
 template <class ReadRange>
 struct RangeReader {
   const std::vector<qsmd5_part>* parts;
   size_t first;
   ReadRange* read;
+  std::atomic<bool> failed{false};
+  std::mutex mu;
   std::exception_ptr err;
+  RangeReader(const std::vector<qsmd5_part>* p, size_t f, ReadRange* r) : parts(p), first(f), read(r) {}
   static uint64_t thunk(void* user, size_t chunk, uint64_t offset, uint64_t len, void* dst) {
     RangeReader* r = static_cast<RangeReader*>(user);
-    if (r->err) return 0;
+    if (r->failed.load(std::memory_order_acquire)) return 0;
     try {
       const qsmd5_part& p = (*r->parts)[r->first + chunk];
       return (uint64_t)(*r->read)(p.offset + offset, (size_t)len, static_cast<char*>(dst));
     } catch (...) {  // never through the C library: carried out below
-      r->err = std::current_exception();
+      std::lock_guard<std::mutex> lk(r->mu);
+      if (!r->err) r->err = std::current_exception();
+      r->failed.store(true, std::memory_order_release);
       return 0;
     }
   }
+  // After the call returned (every library thread is done with thunk).
+  void rethrow_if_failed() {
+    std::exception_ptr e;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      e = err;
+    }
+    if (e) std::rethrow_exception(e);
+  }
+};
+
+// Whether Pool has the non-blocking try_acquire the read-ahead needs (a pool
+// with acquire/release only -- the reference's ResourceManager as it stands --
+// runs the reference's one-buffer loop without read-ahead).
+template <class Pool, class = void>
+struct has_try_acquire : std::false_type {};
+template <class Pool>
+struct has_try_acquire<Pool, decltype((void)std::declval<Pool&>().try_acquire(
+                                 static_cast<typename Pool::buffer_type*>(nullptr)))> : std::true_type {};
+
+template <class Pool>
+bool try_acquire_if_any(Pool& pool, typename Pool::buffer_type* out, std::true_type) {
+  return pool.try_acquire(out);
+}
+template <class Pool>
+bool try_acquire_if_any(Pool&, typename Pool::buffer_type*, std::false_type) {
+  return false;
+}
+
+// One helper thread for the upload loop's read-ahead: at most one read in
+// flight; get() waits for it and rethrows what it threw.
+class ReadAhead {
+ public:
+  ReadAhead() = default;
+  ReadAhead(const ReadAhead&) = delete;
+  ReadAhead& operator=(const ReadAhead&) = delete;
+  ~ReadAhead() {
+    if (!th_.joinable()) return;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    th_.join();
+  }
+  // Starts job on the helper (made on first use); false if no thread could be
+  // made (the caller then reads on its own thread).
+  bool start(std::function<size_t()> job) {
+    if (!th_.joinable()) {
+      try {
+        th_ = std::thread([this] { loop(); });
+      } catch (...) {
+        return false;
+      }
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    job_ = std::move(job);
+    has_job_ = true;
+    done_ = false;
+    err_ = nullptr;
+    cv_.notify_all();
+    return true;
+  }
+  size_t get() {
+    std::unique_lock<std::mutex> lk(mu_);
+    cv_.wait(lk, [&] { return done_; });
+    if (err_) std::rethrow_exception(err_);
+    return got_;
+  }
+
+ private:
+  void loop() {
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || has_job_; });
+      if (stop_ && !has_job_) return;
+      std::function<size_t()> job = std::move(job_);
+      has_job_ = false;
+      lk.unlock();
+      size_t got = 0;
+      std::exception_ptr err;
+      try {
+        got = job();
+      } catch (...) {
+        err = std::current_exception();
+      }
+      lk.lock();
+      got_ = got;
+      err_ = err;
+      done_ = true;
+      cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::thread th_;
+  std::function<size_t()> job_;
+  bool has_job_ = false, done_ = true, stop_ = false;
+  size_t got_ = 0;
+  std::exception_ptr err_;
 };
 
 struct StagedWave {
@@ -482,10 +613,10 @@ StagedWave prehash_wave(const std::vector<qsmd5_part>& parts, size_t first, size
   std::vector<uint64_t> lens(count);
   for (size_t k = 0; k < count; ++k) lens[k] = parts[first + k].size;
   w.dig.resize(16 * count);
-  RangeReader<ReadRange> rr{&parts, first, &read_range, nullptr};
+  RangeReader<ReadRange> rr(&parts, first, &read_range);
   const int rc = qsmd5_hash_read(lens.data(), count, &RangeReader<ReadRange>::thunk, &rr, opt.staging_bytes,
                                  reinterpret_cast<uint8_t(*)[16]>(w.dig.data()), opt.flags | extra_flags);
-  if (rr.err) std::rethrow_exception(rr.err);
+  rr.rethrow_if_failed();
   check(rc, "qsmd5_hash_read");
   w.backend = qsmd5_last_backend();  // this thread's call
   w.hash_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -515,9 +646,11 @@ std::vector<std::string> md5_parts_read(const std::vector<qsmd5_part>& parts, Re
 // wait for a lock this thread holds (PrehashOptions::pipeline).  Stats: waves =
 // pre-hash calls, gpu_waves / cpu_waves by their backend, hash_s = time in
 // them (reads included), upload_s = the upload loop (its own reads included),
-// wait_s = upload time spent waiting for a pre-hash (hashing not hidden).
+// wait_s = upload time spent waiting for a pre-hash (hashing not hidden),
+// and the loop's own split (acquire_s, loop_read_s, upload_call_s, read_ahead).
 // A short read or a hashing failure throws before any part of that wave is
-// uploaded; the pool is never held by the pre-hash.
+// uploaded; the pool is never held by the pre-hash.  The pool needs acquire,
+// release, data and size; try_acquire (optional) enables the read-ahead.
 template <class Pool, class ReadRange, class Upload>
 WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, ReadRange&& read_range,
                               Upload&& upload, const StagedOptions& opt = StagedOptions()) {
@@ -548,6 +681,8 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
     }
   };
   auto stop_requested = [&] { return opt.should_continue && !opt.should_continue(); };
+  const bool read_ahead = opt.pipeline && opt.read_ahead;
+  detail::ReadAhead reader;  // joined on return, after every read it ran was waited for
   const auto tw = clock::now();
   detail::StagedWave cur = prep(0, wave_size(0));
   st.wait_s += secs(tw, clock::now());
@@ -575,17 +710,57 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
     }
     const auto t0 = clock::now();
     size_t k = 0;
+    // the read-ahead in flight: part cur.first + ra_k into ra_buf
+    bool ra_valid = false;
+    size_t ra_k = 0;
+    typename Pool::buffer_type ra_buf = typename Pool::buffer_type();
+    auto drop_read_ahead = [&]() noexcept {
+      if (!ra_valid) return;
+      try {
+        (void)reader.get();
+      } catch (...) {
+      }
+      pool.release(ra_buf);
+      ra_valid = false;
+    };
     try {
       for (; k < n; ++k) {
         if (stop_requested()) break;
         const qsmd5_part& p = parts[cur.first + k];
         // The reference's loop body (QSTransferManager.cpp:609-665): one
-        // buffer, acquired while this thread holds none.
-        typename Pool::buffer_type b = pool.acquire();
-        if (!Pool::data(b)) throw std::runtime_error("transfer buffer pool is shut down: upload stopped");
+        // buffer, acquired while this thread holds none -- or the buffer the
+        // read-ahead already filled with this part.
+        typename Pool::buffer_type b;
+        size_t got = 0;
+        const auto r0 = clock::now();
+        if (ra_valid && ra_k == k) {
+          ra_valid = false;
+          b = ra_buf;
+          try {
+            got = reader.get();
+          } catch (...) {
+            pool.release(b);
+            throw;
+          }
+          st.loop_read_s += secs(r0, clock::now());
+        } else {
+          b = pool.acquire();
+          st.acquire_s += secs(r0, clock::now());
+          if (!Pool::data(b)) throw std::runtime_error("transfer buffer pool is shut down: upload stopped");
+          if (Pool::size(b) < p.size) {
+            pool.release(b);
+            throw std::invalid_argument("pool buffer smaller than a part");
+          }
+          const auto r1 = clock::now();
+          try {
+            got = read_range(p.offset, (size_t)p.size, Pool::data(b));
+          } catch (...) {
+            pool.release(b);
+            throw;
+          }
+          st.loop_read_s += secs(r1, clock::now());
+        }
         try {
-          if (Pool::size(b) < p.size) throw std::invalid_argument("pool buffer smaller than a part");
-          const size_t got = read_range(p.offset, (size_t)p.size, Pool::data(b));
           if (got != p.size)
             throw std::runtime_error("short read of part " + std::to_string(p.part_number) + ": " +
                                      std::to_string(got) + " of " + std::to_string(p.size) + " bytes");
@@ -599,7 +774,28 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
             std::memcpy(&cur.dig[16 * k], d, 16);
             ++st.rehashed;
           }
+          // The next part's read, behind this part's upload, into a buffer
+          // that is free right now (never a blocking acquire while holding b).
+          if (read_ahead && k + 1 < n) {
+            typename Pool::buffer_type b2;
+            const qsmd5_part& q = parts[cur.first + k + 1];
+            if (detail::try_acquire_if_any(pool, &b2, detail::has_try_acquire<Pool>())) {
+              if (Pool::size(b2) >= q.size &&
+                  reader.start([&read_range, q, b2] {
+                    return (size_t)read_range(q.offset, (size_t)q.size, Pool::data(b2));
+                  })) {
+                ra_valid = true;
+                ra_k = k + 1;
+                ra_buf = b2;
+                ++st.read_ahead;
+              } else {
+                pool.release(b2);
+              }
+            }
+          }
+          const auto u0 = clock::now();
           upload(p, b, detail::hex(&cur.dig[16 * k]));
+          st.upload_call_s += secs(u0, clock::now());
         } catch (...) {
           pool.release(b);  // not handed over
           throw;
@@ -608,9 +804,11 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
         ++st.uploaded;
       }
     } catch (...) {
+      drop_read_ahead();
       drain_ahead();
       throw;
     }
+    drop_read_ahead();  // stopped inside the wave: the part read ahead is not uploaded
     st.upload_s += secs(t0, clock::now());
     if (k < n) {
       drain_ahead();

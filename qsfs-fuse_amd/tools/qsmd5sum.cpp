@@ -56,7 +56,8 @@ uint64_t pread_part(void* user, size_t chunk, uint64_t offset, uint64_t len, voi
   while (done < len) {
     const ssize_t got = pread(r.file->fd, static_cast<char*>(dst) + done, len - done,
                               (off_t)(r.offset + offset + done));
-    if (got <= 0) break;  // a short count fails the batch with -EIO
+    if (got < 0 && errno == EINTR) continue;  // interrupted by a signal: not a short read
+    if (got <= 0) break;  // EOF or an error: a short count fails the batch with -EIO
     done += (uint64_t)got;
   }
   return done;

@@ -20,7 +20,7 @@
 //   binding's addition), sync_unflagged (the negative control: the lock held,
 //   the flag not set -- a helper thread's read waits forever; the watchdog
 //   exits 3).  write_after: once that many parts went out, the file is
-//   written (the next part to go out changes) as by another descriptor.
+//   written (the part after the next to go out changes) as by another descriptor.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -236,8 +236,10 @@ int main(int argc, char** argv) {
   up.write_after = argc > 6 ? atoi(argv[6]) : -1;
   if (up.write_after >= 0) {
     up.writer = &file;
-    // the next part to go out: already pre-hashed (its wave is the one uploading)
-    const qsmd5_part& next = plan[std::min<size_t>(up.write_after, plan.size() - 1)];
+    // the part after the next one to go out: already pre-hashed (its wave is
+    // the one uploading) and not yet read into a buffer (the next one may be:
+    // the loop's read-ahead reads it while this part uploads)
+    const qsmd5_part& next = plan[std::min<size_t>(up.write_after + 1, plan.size() - 1)];
     up.write_off = next.offset + next.size / 2;
   }
   up.rm = make_shared<ResourceManager>(pool_n, largest);

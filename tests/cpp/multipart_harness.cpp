@@ -28,6 +28,17 @@
 // qsmd5::upload_parts_staged pulls every part through qsmd5_hash_read in column
 // windows (--staging=BYTES budget, --wave-parts=W parts per call, default the
 // whole file), then runs the reference's loop one pool buffer at a time.
+// --reference-loop replaces all of it with the reference's own flush loop, the
+// baseline the staged binding is timed against: per part,
+// Acquire one pool buffer (blocking), ReadNoLoad into it, md5() of the
+// IOStream over its first part.size bytes with the REFERENCE's MD5.cpp
+// (oracle/_ref/libref_md5.so, ref_md5_iostream = md5(shared_ptr<iostream>),
+// MD5.cpp:341-349 -- test infrastructure, dlopen'd only in this mode), then the
+// upload; on this thread (File::Flush's async = false) or, with --async=E, md5
+// and upload both on the executor, as UploadMultipart computes the digest
+// inside MultipleUploadWrapper (QSTransferManager.cpp:602-673, QSClient.cpp:369-371).
+// --read-parallel: the pre-hash's reads on QSMD5_READ_THREADS library threads
+// (QSMD5_FLAG_READ_PARALLEL; this file's page gather is thread-safe).
 // File content: part-aligned mode (--aligned) makes part i = LCG(12345 + i),
 // the parts of tests/golden/batch_10MiB.json, for every file; otherwise file f
 // is one LCG(seed + f) stream.  Prints one JSON object with the digests in
@@ -38,6 +49,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <dirent.h>
+#include <dlfcn.h>
+#include <limits.h>
 #include <pthread.h>
 #include <sched.h>
 #include <sys/resource.h>
@@ -309,6 +322,71 @@ qsmd5::WaveStats naive_upload(const std::vector<qsmd5_part>& parts, WatchedPool&
   return st;
 }
 
+// The reference's md5(shared_ptr<iostream>) from oracle/_ref/libref_md5.so
+// (built from /root/reference/src/base/MD5.cpp by oracle/build_ref.sh), found
+// next to this binary's tree.
+typedef void (*ref_md5_fn)(const char* p, uint64_t len, char out[33]);
+ref_md5_fn load_reference_md5() {
+  char exe[PATH_MAX];
+  const ssize_t m = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+  if (m <= 0) return nullptr;
+  exe[m] = 0;
+  std::string dir(exe);
+  dir = dir.substr(0, dir.rfind('/'));  // tests/cpp
+  const std::string so = dir + "/../../oracle/_ref/libref_md5.so";
+  void* h = dlopen(so.c_str(), RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    fprintf(stderr, "--reference-loop: %s\n", dlerror());
+    return nullptr;
+  }
+  return reinterpret_cast<ref_md5_fn>(dlsym(h, "ref_md5_iostream"));
+}
+
+// QSTransferManager::DoMultiPartUpload with -m, as the reference runs it.
+// Sync: acquire, read, md5, upload, release per part on this thread.  Async:
+// acquire and read here, then the executor runs md5 + upload and releases.
+template <class Upload>
+qsmd5::WaveStats reference_upload(const std::vector<qsmd5_part>& parts, WatchedPool& pool,
+                                  const PagedFile& file, ref_md5_fn ref_md5, bool async,
+                                  std::atomic<double>* exec_hash_s, Upload&& upload) {
+  using clock = clock_type;
+  auto secs = [](clock::time_point a, clock::time_point b) {
+    return std::chrono::duration<double>(b - a).count();
+  };
+  qsmd5::WaveStats st;
+  st.waves = st.parts = parts.size();
+  st.cpu_waves = parts.size();
+  for (const qsmd5_part& p : parts) {
+    const auto a0 = clock::now();
+    qsmd5::PoolBuffer b = pool.acquire();
+    const auto a1 = clock::now();
+    st.acquire_s += secs(a0, a1);
+    if (!b.data) throw std::runtime_error("transfer buffer pool is shut down: upload stopped");
+    const size_t got = file.read(p.offset, p.size, b.data);
+    const auto a2 = clock::now();
+    st.loop_read_s += secs(a1, a2);
+    if (got != p.size) {
+      pool.release(b);
+      throw std::runtime_error("short read of part " + std::to_string(p.part_number));
+    }
+    if (!async) {
+      char hex[33];
+      ref_md5(b.data, p.size, hex);
+      const auto a3 = clock::now();
+      st.hash_s += secs(a2, a3);
+      upload(p, b, std::string(hex), false);
+      st.upload_call_s += secs(a3, clock::now());
+      pool.release(b);
+    } else {
+      upload(p, b, std::string(), true);  // the executor hashes, uploads, releases
+      st.upload_call_s += secs(a2, clock::now());
+    }
+    ++st.uploaded;
+  }
+  (void)exec_hash_s;
+  return st;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -316,6 +394,8 @@ int main(int argc, char** argv) {
   size_t pool_n = 5, files = 1, naive_wave = 0, max_wave = 0;
   bool aligned = false, pinned = false, slab = false, reg = false, pipeline = true, staged = false;
   bool foreground = false;  // --foreground: StagedOptions::background_waves = false
+  bool reference_loop = false, read_ahead = true;
+  bool read_parallel = false;  // --read-parallel: the pre-hash's reads on QSMD5_READ_THREADS threads
   uint64_t staging = 0;
   size_t wave_parts = 0, first_wave = 0;
   size_t cpus = 0, load_threads = 0;  // --cpus: the process's cores; --load: spinning threads on them
@@ -350,6 +430,9 @@ int main(int argc, char** argv) {
     else if (const char* v = val("--cpus=")) cpus = strtoull(v, nullptr, 0);
     else if (const char* v = val("--load=")) load_threads = strtoull(v, nullptr, 0);
     else if (a == "--staged") staged = true;
+    else if (a == "--reference-loop") reference_loop = true;
+    else if (a == "--no-read-ahead") read_ahead = false;
+    else if (a == "--read-parallel") read_parallel = true;
     else if (a == "--foreground") foreground = true;
     else if (a == "--aligned") aligned = true;
     else if (a == "--pinned") pinned = true;
@@ -365,6 +448,12 @@ int main(int argc, char** argv) {
     fprintf(stderr, "--pool must be >= 1\n");
     return 2;
   }
+  ref_md5_fn ref_md5 = nullptr;
+  if (reference_loop && !(ref_md5 = load_reference_md5())) {
+    fprintf(stderr, "--reference-loop needs oracle/_ref/libref_md5.so (oracle/build_ref.sh)\n");
+    return 2;
+  }
+  std::atomic<double> exec_hash_s{0};  // --reference-loop --async: md5 time on the executor
   // --cpus=C: a daemon held to C cores (the first C of its allowed set), set
   // before any thread -- the library's and HIP's included -- is created, so
   // every thread inherits it.
@@ -480,6 +569,7 @@ int main(int argc, char** argv) {
   std::vector<std::string> errors(files);
   double total = 0;
   for (int rep = 0; rep < repeat; ++rep) {
+    exec_hash_s.store(0);  // per pass, as st[] below
     const auto t0 = clock_type::now();
     const double c0 = cpu_seconds();
     std::vector<std::thread> th;
@@ -490,6 +580,39 @@ int main(int argc, char** argv) {
         try {
           if (naive_wave) {
             st[f] = naive_upload(parts, shared, pf, naive_wave, upload_ms, &md5[f]);
+            return;
+          }
+          if (reference_loop) {
+            InFlight inflight;
+            auto up = [&](const qsmd5_part& p, const qsmd5::PoolBuffer& b, const std::string& hex, bool async) {
+              if (!async) {
+                sleep_ms(upload_ms);
+                md5[f][p.part_number - 1] = hex;
+                progress();
+                return;
+              }
+              inflight.add();
+              exec->submit([&, p, b] {
+                char h[33];
+                const auto h0 = clock_type::now();
+                ref_md5(b.data, p.size, h);  // md5(buffer) inside UploadMultipart
+                double cur = exec_hash_s.load();
+                const double d = std::chrono::duration<double>(clock_type::now() - h0).count();
+                while (!exec_hash_s.compare_exchange_weak(cur, cur + d)) {
+                }
+                sleep_ms(upload_ms);
+                md5[f][p.part_number - 1] = h;
+                shared.release(b);
+                inflight.done();
+              });
+            };
+            try {
+              st[f] = reference_upload(parts, shared, pf, ref_md5, exec != nullptr, &exec_hash_s, up);
+            } catch (...) {
+              inflight.wait();
+              throw;
+            }
+            inflight.wait();
             return;
           }
           qsmd5::PrehashOptions opt;
@@ -546,6 +669,8 @@ int main(int argc, char** argv) {
               so.pipeline = pipeline;
               so.upload_releases = opt.upload_releases;
               so.should_continue = opt.should_continue;
+              so.read_ahead = read_ahead;
+              if (read_parallel) so.flags |= QSMD5_FLAG_READ_PARALLEL;  // PagedFile::read is const: thread-safe
               st[f] = qsmd5::upload_parts_staged(parts, shared, read_range, upload, so);
             } else {
               st[f] = qsmd5::upload_parts_prehashed(parts, shared, read, upload, opt);
@@ -610,7 +735,12 @@ int main(int argc, char** argv) {
     sum.hash_s += s.hash_s;
     sum.upload_s += s.upload_s;
     sum.wait_s += s.wait_s;
+    sum.acquire_s += s.acquire_s;
+    sum.loop_read_s += s.loop_read_s;
+    sum.upload_call_s += s.upload_call_s;
+    sum.read_ahead += s.read_ahead;
   }
+  if (reference_loop && exec) sum.hash_s += exec_hash_s.load();
   auto md5_list = [&](const std::vector<std::string>& v) {
     std::string s = "[";
     for (size_t i = 0; i < v.size(); ++i) s += std::string(i ? ", " : "") + "\"" + v[i] + "\"";
@@ -634,6 +764,9 @@ int main(int argc, char** argv) {
   printf("], \"cpus\": %zu, \"load_threads\": %zu, \"cpu_efficiency\": %.4f, \"wave_parts\": %zu, \"first_wave\": %zu, "
          "\"background_waves\": %s, \"rehashed\": %zu",
          cpus, load_threads, cpu_eff, wave_parts, first_wave, foreground ? "false" : "true", sum.rehashed);
+  printf(", \"reference_loop\": %s, \"read_ahead\": %zu, \"acquire_s\": %.6f, \"loop_read_s\": %.6f, "
+         "\"upload_call_s\": %.6f", reference_loop ? "true" : "false", sum.read_ahead, sum.acquire_s,
+         sum.loop_read_s, sum.upload_call_s);
   printf(", \"busy_threads\": {%s}, \"cpu_s_runs\": [", busy_threads().c_str());
   for (size_t i = 0; i < cpu_runs.size(); ++i) printf("%s%.6f", i ? ", " : "", cpu_runs[i]);
   printf("], \"md5\": %s, \"md5_files\": [", md5_list(md5[0]).c_str());

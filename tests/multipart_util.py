@@ -24,7 +24,7 @@ def build():
         subprocess.check_call(["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", src,
                                "-I" + os.path.join(ROOT, "include"),
                                "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
-                               "-lpthread", "-Wl,-rpath,$ORIGIN/../../qsfs-fuse_amd/lib", "-o", HARNESS])
+                               "-lpthread", "-ldl", "-Wl,-rpath,$ORIGIN/../../qsfs-fuse_amd/lib", "-o", HARNESS])
 
 
 def run_raw(args, backend, timeout=300, extra_env=None):
@@ -55,6 +55,6 @@ def build_tsan():
         subprocess.check_call(["/opt/rocm/llvm/bin/clang++", "-std=c++17", "-O1", "-g",
                                "-fsanitize=thread", src, "-I" + os.path.join(ROOT, "include"),
                                "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
-                               "-lpthread", "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"),
+                               "-lpthread", "-ldl", "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"),
                                "-o", HARNESS_TSAN])
     return HARNESS_TSAN

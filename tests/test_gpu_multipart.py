@@ -13,7 +13,7 @@ import os
 
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, ROOT
 from multipart_util import run
 
 torch = pytest.importorskip("torch")
@@ -139,3 +139,24 @@ def test_concurrent_files_gpu_waves(gold, mode):
     assert r["pool_free_after"] == 32 and r["gpu_waves"] >= 4 and r["cpu_waves"] == 0, r
     for m in r["md5_files"]:
         assert m[:want] == gold[:want] and not any(m[want:]), m
+
+
+def test_reference_loop_beside_the_staged_binding():
+    """the flush loop the binding replaces, timed beside it
+    on the same file -- QSTransferManager::DoMultiPartUpload with -m as the
+    reference runs it (Acquire, ReadNoLoad, the reference's own
+    md5(shared_ptr<iostream>) from oracle/_ref, upload; serial on the flushing
+    thread) against qsmd5::upload_parts_staged, 128 x 10 MiB at -n 5, uploads
+    that return at once.  Both golden; the binding is faster."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "libref_md5.so")):
+        pytest.skip("oracle/_ref not built")
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    base = ["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=5"]
+    ref = run(base + ["--reference-loop"], "auto", timeout=600)
+    stg = run(base + ["--pinned", "--staged", "--repeat=2"], "gpu", timeout=600)
+    assert ref["md5"] == gold[:128] and stg["md5"] == gold[:128]
+    rw, sw = ref["seconds"], min(stg["wall_s_runs"])
+    print("128 x 10 MiB, -n 5: reference loop %.3f s (md5 %.3f s, reads %.3f s, %.2f CPU-s); "
+          "staged binding %.3f s (%.2f CPU-s): %.1fx" % (rw, ref["hash_s"], ref["loop_read_s"],
+                                                        ref["cpu_s_runs"][0], sw, stg["cpu_s_runs"][-1], rw / sw))
+    assert sw < rw

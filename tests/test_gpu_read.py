@@ -282,3 +282,99 @@ def test_read_parallel_flag_on_the_gpu(golden, monkeypatch):
     got = qsmd5.hash_read([L] * 512, rd, flags=GPU | qsmd5.FLAG_READ_PARALLEL)
     assert [d.hex() for d in got] == gold
     rd.check_contract()
+
+
+# ---- round 6 ---------------------------------------------------------------------
+
+def _harness_golden(r, parts):
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    assert all(m == gold[:parts] for m in r["md5_files"])
+
+
+@pytest.mark.cpu_backend
+@pytest.mark.parametrize("parts", [128, 512])
+def test_auto_prehash_matches_forced_gpu(parts):
+    """the whole-file pre-hash (qsfs's -n 5 pool, the
+    staged binding) under the default auto routing must run as fast as forced
+    GPU whenever auto picks the GPU: within 5% on the best of four passes,
+    every digest golden.  Round 5's gap was the read slot's buffers (65-80 ms
+    of pinned and device allocation) landing in the first GPU job, which
+    under auto often follows CPU-routed ones; they are now made at init.
+    Forced CPU runs too, and auto's best pass is within 15% of the faster
+    backend's.  QSMD5_TRACE=1 shows where each call's time went."""
+    args = ["--aligned", "--size=%d" % (parts * 10 * MiB), "--pool=5", "--pinned", "--staged", "--repeat=4"]
+    best, picks = {}, {}
+    for backend in ("gpu", "cpu", "auto"):
+        r = run(args, backend, timeout=600, extra_env={"QSMD5_TRACE": "1"})
+        _harness_golden(r, parts)
+        traces = [json.loads(l.split("qsmd5 read trace: ", 1)[1]) for l in r["_stderr"].splitlines()
+                  if "qsmd5 read trace: " in l]
+        assert len(traces) == 4
+        picks[backend] = traces
+        best[backend] = min(t["total_ms"] for t in traces)
+        print("%s %d parts: pre-hash calls %s" % (backend, parts, [
+            (t["backend"], t["reason"], round(t["total_ms"], 1), round(t["read_ms"], 1)) for t in traces]))
+    auto_gpu = [t["total_ms"] for t in picks["auto"] if t["backend"] == "gpu"]
+    if auto_gpu:
+        assert min(auto_gpu) <= 1.05 * best["gpu"], (min(auto_gpu), best["gpu"])
+    assert best["auto"] <= 1.15 * min(best["gpu"], best["cpu"]), best
+
+
+def _nested_exe(tmp_path):
+    import subprocess
+    from conftest import ROOT
+    exe = str(tmp_path / "nested_read")
+    subprocess.check_call([
+        "g++", "-std=c++17", "-O2", os.path.join(ROOT, "tests", "cpp", "nested_read.cpp"),
+        "-I" + os.path.join(ROOT, "include"), "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
+        "-lpthread", "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-o", exe])
+    return exe
+
+
+@pytest.mark.cpu_backend
+@pytest.mark.parametrize("args,slots", [(["nested-read", "gpu", "auto"], "1"),
+                                        (["nested-read", "gpu", "gpu"], "1"),
+                                        (["nested-read", "gpu", "gpu"], "2"),
+                                        (["shutdown", "gpu"], "4")])
+def test_read_callbacks_call_back_into_the_library_on_the_gpu(tmp_path, args, slots):
+    """ADVICE r05 on the box: the outer batch hashes on the GPU and holds a
+    read slot through its read callbacks.  A nested qsmd5_hash_read from a
+    callback takes the CPU path under auto (no slot needed); forced onto the
+    GPU it takes a free slot if there is one (QSMD5_READ_SLOTS=2) and
+    returns -EDEADLK when the outer batch holds the only one -- never a
+    deadlock.  With parallel readers a shutdown pending meanwhile waits for
+    the outer batch, whose reader threads' nested calls pass the gate."""
+    import subprocess
+    env = dict(os.environ, QSMD5_BACKEND="auto", QSMD5_READ_SLOTS=slots)
+    out = subprocess.run([_nested_exe(tmp_path)] + args, capture_output=True, text=True, timeout=120, env=env)
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0 and r["deadlock"] is False and r["digests_ok"], out.stdout + out.stderr
+    assert r["backend"] == qsmd5.BACKEND_GPU
+    if args[0] == "nested-read":
+        if args[2] == "gpu" and slots == "1":
+            assert r["nested_edeadlk"] == r["nested_calls"] > 0
+        else:
+            assert r["nested_ok"] == r["nested_calls"] > 0
+    print(r)
+
+
+def test_parallel_readers_prehash_rate():
+    """the pull-driven pre-hash of 512 x 10 MiB parts
+    gathered from a paged file, with 1 and 4 reader threads, the window copy
+    and the column kernel overlapped on two streams (default) or in one stream
+    (QSMD5_READ_OVERLAP=0, round 5).  Prints the rates; every digest golden."""
+    args = ["--aligned", "--size=%d" % (512 * 10 * MiB), "--pool=5", "--pinned", "--staged", "--repeat=3"]
+    rates = {}
+    for readers in (1, 4):
+        for overlap in ("1", "0"):
+            extra = ["--read-parallel"] if readers > 1 else []
+            r = run(args + extra, "gpu", timeout=600,
+                    extra_env={"QSMD5_TRACE": "1", "QSMD5_READ_THREADS": str(readers), "QSMD5_READ_OVERLAP": overlap})
+            _harness_golden(r, 512)
+            traces = [json.loads(l.split("qsmd5 read trace: ", 1)[1]) for l in r["_stderr"].splitlines()
+                      if "qsmd5 read trace: " in l]
+            best = min(traces, key=lambda t: t["total_ms"])
+            rates[(readers, overlap)] = 5.0 / (best["total_ms"] / 1e3)
+            print("readers %d overlap %s: %.1f GiB/s (read %.1f ms, region waits %.1f ms, tail %.1f ms)"
+                  % (readers, overlap, rates[(readers, overlap)], best["read_ms"], best["region_wait_ms"],
+                     best["tail_ms"]))

@@ -285,3 +285,83 @@ def test_busy_cores_lower_the_cpu_efficiency():
     assert busy["cpus"] == 2 and busy["load_threads"] == 2
     assert busy["cpu_efficiency"] < 0.75, busy["cpu_efficiency"]
     assert busy["cpu_efficiency"] < idle["cpu_efficiency"] - 0.2, (idle["cpu_efficiency"], busy["cpu_efficiency"])
+
+
+# ---- round 6: the reference's own loop beside the staged binding, read-ahead ------
+
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_md5.so")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref not built (oracle/build_ref.sh)")
+@pytest.mark.parametrize("mode", [[], ["--async=5"]])
+def test_reference_loop_matches_golden(mode):
+    """--reference-loop (VERDICT r05 item 1): QSTransferManager::DoMultiPartUpload
+    with -m as the reference runs it -- Acquire, ReadNoLoad, the reference's own
+    md5(shared_ptr<iostream>) from oracle/_ref (MD5.cpp compiled in place; the
+    baseline, test infrastructure), upload -- on the flushing thread or on the
+    executor.  Its digests are the golden table's, so the staged binding and
+    the loop it replaces are timed on the same bytes."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    r = run(["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5", "--reference-loop", "--upload-ms=1"] + mode,
+            "cpu")
+    assert r["reference_loop"] is True and r["md5"] == gold[:12] and r["uploaded"] == 12
+    assert r["pool_free_after"] == 5 and r["hash_s"] > 0
+    if not mode:  # serial: every part's md5 on this thread, between its read and its upload
+        assert r["seconds"] >= r["hash_s"] + r["loop_read_s"]
+
+
+@pytest.mark.parametrize("extra", [[], ["--async=3"], ["--wave-parts=5", "--first-wave=2"]])
+def test_staged_read_ahead_matches_golden(extra):
+    """StagedOptions::read_ahead (VERDICT r05 item 3): the next part is read
+    into a buffer the pool has free (try_acquire) while this part uploads; the
+    digests stay golden, every buffer comes back, and nearly every part after
+    each wave's first was read ahead.  --no-read-ahead is the reference's
+    one-buffer loop exactly."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    base = ["--aligned", "--size=%d" % (16 * 10 * MiB), "--pool=5", "--staged", "--upload-ms=2"] + extra
+    on = run(base, "cpu")
+    off = run(base + ["--no-read-ahead"], "cpu")
+    for r in (on, off):
+        assert r["md5"] == gold[:16] and r["uploaded"] == 16 and r["pool_free_after"] == 5
+    assert off["read_ahead"] == 0 and on["read_ahead"] >= 16 - on["waves"] - 2, on["read_ahead"]
+
+
+def test_staged_read_ahead_faults_return_every_buffer():
+    """A short read that the read-ahead hits, and a failing upload while a part
+    is being read ahead: the upload stops, nothing leaks."""
+    for fault, want in (("--short-read-part=7", 0), ("--fail-upload-part=7", 6)):
+        out = run_raw(["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5", "--staged", "--wave-parts=12",
+                       fault], "cpu")
+        assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+        r = json.loads(out.stdout)
+        assert r["uploaded"] == want and r["pool_free_after"] == 5, (fault, r["uploaded"])
+
+
+def _nested_read_exe(tmp_path):
+    exe = str(tmp_path / "nested_read")
+    subprocess.check_call([
+        "g++", "-std=c++17", "-O2", os.path.join(ROOT, "tests", "cpp", "nested_read.cpp"),
+        "-I" + os.path.join(ROOT, "include"), "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5",
+        "-lpthread", "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-o", exe])
+    return exe
+
+
+@pytest.mark.parametrize("args", [["shutdown", "cpu"], ["nested-read", "cpu", "auto"],
+                                  ["nested-read", "cpu", "cpu"]])
+def test_read_callbacks_call_back_into_the_library(tmp_path, args):
+    """read callbacks that call qsmd5 entry points.  With
+    QSMD5_FLAG_READ_PARALLEL the callbacks also run on the library's reader
+    threads; one of them starts qsmd5_shutdown and then calls qsmd5_hash_one
+    while the shutdown is pending.  A reader thread's call is a nested call
+    (its depth is raised), so it does not wait at the shutdown gate: the
+    outer call finishes and the shutdown then gets through.  (Round 5's
+    reader threads deadlocked here: outer call, reader thread and shutdown
+    waiting on each other.)  Nested qsmd5_hash_read calls hash right too."""
+    out = subprocess.run([_nested_read_exe(tmp_path)] + args, capture_output=True, text=True, timeout=120,
+                         env=dict(os.environ, QSMD5_BACKEND="auto"))
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    assert out.returncode == 0 and r["deadlock"] is False and r["digests_ok"], out.stdout + out.stderr
+    if args[0] == "shutdown":
+        assert r["reader_thread_reads"] > 0 and r["shutdown_rc"] == 0
+    else:
+        assert r["nested_ok"] == r["nested_calls"] > 0

@@ -164,14 +164,18 @@ def test_read_lanes_and_scalar_agree(monkeypatch, threads, staging):
 
 
 def test_read_routing_compares_wall_times(monkeypatch):
-    """Round 5: auto routes a pull-driven batch by its wall time on each
-    backend, max(the caller's reads, the hashing), since both overlap the
-    reads with the hashing.  With reads priced fast (QSMD5_READ_GIBS=50), 8 x
-    10 MiB prices to the CPU lanes (~23 ms) against one GPU chain (~85 ms);
-    with reads priced slow (0.5 GiB/s) both backends are read-bound, the tie
-    goes to the GPU (whose hashing leaves the host's cores free) -- here,
-    without a GPU, that attempt falls back to the CPU.  The log carries the
-    decision."""
+    """Auto routes a pull-driven batch by its wall time on each backend:
+    the reads and the hashing overlap window by window, so it is about
+    max(the caller's reads, the hashing), plus on the GPU the last window's
+    copy and column kernel (round 6).  With reads priced fast
+    (QSMD5_READ_GIBS=50), 8 x 10 MiB prices to the CPU lanes (~23 ms) against
+    one GPU chain (~85 ms); with reads priced slow (0.5 GiB/s) and narrow
+    windows (a 2 MiB budget: 128 KiB columns, a ~1 ms GPU tail) both backends
+    are read-bound and the GPU is within 5% of the CPU, which routes it to
+    the GPU (whose hashing leaves the host's cores free) -- here, without a
+    GPU, that attempt falls back to the CPU.  With the default budget the
+    10 MiB columns leave no overlap (one window: read it all, then an 85 ms
+    chain) and the CPU wins.  The log carries the decision."""
     if qsmd5.device_count() > 0:
         pytest.skip("GPU present: the slow-read case would really run on it")
     if "avx512f" not in open("/proc/cpuinfo").read():
@@ -185,11 +189,12 @@ def test_read_routing_compares_wall_times(monkeypatch):
         lens = [10 * MiB] * 8
         bufs = [lcg_bytes(77 + i, L) for i, L in enumerate(lens)]
         want_md5 = md5_many([(b, L) for b, L in zip(bufs, lens)])
-        for gibs, want in (("50", "backend=cpu reason=size"), ("0.5", "backend=gpu reason=size")):
+        for gibs, staging, want in (("50", 0, "backend=cpu reason=size"), ("0.5", 2 * MiB, "backend=gpu reason=size"),
+                                    ("0.5", 0, "backend=cpu reason=size")):
             monkeypatch.setenv("QSMD5_READ_GIBS", gibs)
             del lines[:]
-            assert qsmd5.hash_read(lens, Recorder(bufs, lens)) == want_md5  # auto: no flags
-            assert any(want in l and "(read)" in l for l in lines), (gibs, lines)
+            assert qsmd5.hash_read(lens, Recorder(bufs, lens), staging_bytes=staging) == want_md5  # auto
+            assert any(want in l and "(read)" in l for l in lines), (gibs, staging, lines)
     finally:
         qsmd5.set_log_callback(None)
 
