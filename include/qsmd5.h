@@ -301,7 +301,7 @@ QSMD5_API int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t
  *   read(user, chunk, offset, len, dst): copy bytes [offset, offset + len) of
  *   chunk `chunk` (0-based index into lens) to dst and return the number of
  *   bytes copied, as ReadNoLoad's readSize.  Any other count than len fails the
- * *   call with -EIO (the reference stops the upload on a short read,
+ *   call with -EIO (the reference stops the upload on a short read,
  *   QSTransferManager.cpp:625-643); nothing is hashed from it.
  *
  * read runs on the calling thread only (QSMD5_FLAG_READ_PARALLEL: on several
@@ -310,14 +310,20 @@ QSMD5_API int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t
  * asked for once --
  * except that in QSMD5_BACKEND=auto a GPU failure re-runs the whole batch on
  * the CPU, asking for every byte again from offset 0.  It may call other qsmd5
- * entry points (not qsmd5_shutdown).  lens[i] < 2^38.  Routed like
- * qsmd5_hash_batch_ex (flags: QSMD5_FLAG_GPU_ONLY / _CPU_ONLY /
- * _REF_TRUNCATE32).  Calls from different threads (files flushed at once)
- * run side by side, each with its own stream and staging, up to
- * QSMD5_READ_SLOTS per GPU at a time (default 4, at most 8; each slot holds
- * up to staging_bytes of pinned host memory (two regions) and staging_bytes / 2
- * of HBM, taken on first use and kept until qsmd5_shutdown); a further call
- * waits for a slot.  One bound GPU
+ * entry points (not qsmd5_shutdown), on any of those threads.  A nested
+ * qsmd5_hash_read (from inside read) never waits for a read slot, as the
+ * outer call holds one through its reads: under auto routing it runs on the
+ * CPU; under QSMD5_FLAG_GPU_ONLY it takes a free slot or returns -EDEADLK.
+ * lens[i] < 2^38.  Routed like qsmd5_hash_batch_ex (flags:
+ * QSMD5_FLAG_GPU_ONLY / _CPU_ONLY / _REF_TRUNCATE32), by the wall time of
+ * the reads and the hashing on each backend.  Calls from different threads
+ * (files flushed at once) run side by side, each with its own streams and
+ * staging, up to QSMD5_READ_SLOTS per GPU at a time (default 4, at most 8;
+ * each slot holds up to staging_bytes of pinned host memory and as much HBM,
+ * split into QSMD5_READ_REGIONS regions (default 2); slot 0 of the primary
+ * GPU is taken at initialisation unless QSMD5_READ_PREWARM=0, the others on
+ * first use, all kept until qsmd5_shutdown); a further call waits for a
+ * slot.  One bound GPU
  * hashes a whole call: the one with the fewest such calls in flight (the
  * first on a tie), so with QSMD5_DEVICES binding several, files flushed at
  * once spread over the GPUs. */

@@ -427,10 +427,18 @@ struct StagedOptions {
   // and each larger wave is pre-hashed while the smaller one before it uploads.
   size_t first_wave_parts = 0;
   // With pipeline: the waves after the first are pre-hashed while the one
-  // before them uploads, so their latency is hidden; they go out with
+  // before them uploads.  Where that hides their latency they go out with
   // QSMD5_FLAG_BACKGROUND (the GPU whenever one is usable, leaving the host's
-  // cores to the daemon's own threads).  The first wave, which the first
-  // upload waits for, is routed for speed.  false: every wave for speed.
+  // cores to the daemon's own threads): when the wave uploading meanwhile,
+  // at the upload loop's own measured pace per part so far, lasts at least
+  // 1.25 x the next wave's GPU time (its longest part's chain at the
+  // library's GPU chain rate, qsmd5_get_rates, plus its bytes read at 12
+  // GiB/s).  Otherwise -- the first wave, which the first upload waits for,
+  // a wave behind one too short to hide it, and every wave when uploads
+  // return at once -- the wave is routed for speed.  Round 5 sent every wave
+  // after the first to the GPU: behind the ramp's 4-part first wave the
+  // 8-part second one (one ~85 ms chain) outlasted 40 ms of uploads and the
+  // uploader waited.  false: every wave for speed.
   bool background_waves = true;
   bool pipeline = true;        // pre-hash the next wave on a helper thread while this one uploads
                                // (read_range then runs there too: PrehashOptions::pipeline)
@@ -667,10 +675,26 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
     if (!opt.first_wave_parts || !opt.wave_parts || !opt.pipeline) return per;
     return prev ? std::min(per, 2 * prev) : std::min(per, opt.first_wave_parts);
   };
-  auto prep = [&](size_t first, size_t count) {
-    // a wave pre-hashed behind an upload (not the first) may take its time
-    const int extra = (first > 0 && opt.pipeline && opt.background_waves) ? QSMD5_FLAG_BACKGROUND : 0;
-    return detail::prehash_wave(parts, first, std::min(count, parts.size() - first), read_range, opt, extra);
+  auto prep = [&](size_t first, size_t count, bool background) {
+    return detail::prehash_wave(parts, first, std::min(count, parts.size() - first), read_range, opt,
+                                background ? QSMD5_FLAG_BACKGROUND : 0);
+  };
+  // Whether the wave [first, first + count) is hidden behind `uploading`
+  // parts' uploads (StagedOptions::background_waves).
+  double loop_s = 0;  // the upload loop's time so far, and the parts it uploaded
+  size_t loop_parts = 0;
+  auto hidden = [&](size_t first, size_t count, size_t uploading) {
+    if (!(opt.pipeline && opt.background_waves) || first == 0 || loop_parts == 0) return false;
+    qsmd5_rates r;
+    if (qsmd5_get_rates(&r) != 0 || r.gpu_chain_gibs <= 0) return false;
+    uint64_t longest = 0, total = 0;
+    for (size_t i = first; i < std::min(parts.size(), first + count); ++i) {
+      longest = std::max<uint64_t>(longest, parts[i].size);
+      total += parts[i].size;
+    }
+    const double gib = 1073741824.0;
+    const double gpu_s = (double)longest / (r.gpu_chain_gibs * gib) + (double)total / (12.0 * gib);
+    return (double)uploading * (loop_s / (double)loop_parts) >= 1.25 * gpu_s;
   };
   std::future<detail::StagedWave> ahead;
   auto drain_ahead = [&]() noexcept {
@@ -684,7 +708,7 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
   const bool read_ahead = opt.pipeline && opt.read_ahead;
   detail::ReadAhead reader;  // joined on return, after every read it ran was waited for
   const auto tw = clock::now();
-  detail::StagedWave cur = prep(0, wave_size(0));
+  detail::StagedWave cur = prep(0, wave_size(0), false);
   st.wait_s += secs(tw, clock::now());
   for (;;) {
     if (cur.cancelled) {
@@ -703,12 +727,13 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
     }
     if (opt.pipeline && next < parts.size()) {
       try {
-        ahead = std::async(std::launch::async, prep, next, wave_size(n));
+        ahead = std::async(std::launch::async, prep, next, wave_size(n), hidden(next, wave_size(n), n));
       } catch (...) {
         // no thread or no memory for one: the next wave is pre-hashed here, after this one
       }
     }
     const auto t0 = clock::now();
+    const size_t uploaded0 = st.uploaded;
     size_t k = 0;
     // the read-ahead in flight: part cur.first + ra_k into ra_buf
     bool ra_valid = false;
@@ -810,6 +835,8 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
     }
     drop_read_ahead();  // stopped inside the wave: the part read ahead is not uploaded
     st.upload_s += secs(t0, clock::now());
+    loop_s += secs(t0, clock::now());
+    loop_parts += st.uploaded - uploaded0;
     if (k < n) {
       drain_ahead();
       st.stopped = true;
@@ -817,7 +844,7 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
     }
     if (next >= parts.size()) break;
     const auto t1 = clock::now();
-    cur = ahead.valid() ? ahead.get() : prep(next, wave_size(n));
+    cur = ahead.valid() ? ahead.get() : prep(next, wave_size(n), false);
     st.wait_s += secs(t1, clock::now());
   }
   st.wall_s = secs(t_start, clock::now());

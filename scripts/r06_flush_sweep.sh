@@ -53,6 +53,12 @@ for P in ${PARTS:-128 512}; do
       run "staged_whole_u${U}_P$P" --size=$S --pool=5 --pinned --staged --upload-ms=$U --repeat=2 || exit 1
     done
   fi
+  if [[ $CASES == all || $CASES == *files* ]] && [[ $P == 128 ]]; then
+    # four files flushed at once from four threads through one 5-buffer pool
+    run "staged_4files_ramp_u0_P$P" --size=$S --pool=5 --pinned --staged --files=4 --wave-parts=32 --repeat=2 || exit 1
+    run "staged_4files_whole_u0_P$P" --size=$S --pool=5 --pinned --staged --files=4 --repeat=2 || exit 1
+    run "reference_sync_4files_u0_P$P" --size=$S --pool=5 --reference-loop --files=4 || exit 1
+  fi
   if [[ $CASES == all || $CASES == *rate* ]]; then
     # the pre-hash's own rate with 1 and 4 readers, copy/kernel overlapped or
     # in one stream, over 2..4 staging regions; forced
@@ -63,7 +69,7 @@ for P in ${PARTS:-128 512}; do
         --size=$S --pool=5 --pinned --staged --repeat=3 $RP || exit 1
       for G in 2 3 4; do
         QSMD5_READ_THREADS=$R QSMD5_READ_REGIONS=$G BACKEND=gpu run "prehash_readers${R}_overlap1_regions${G}_P$P" \
-          --size=$S --pool=5 --pinned --staged --repeat=3 $RP || exit 1
+          --size=$S --pool=5 --pinned --staged --repeat=5 $RP || exit 1
       done
     done
   fi

@@ -196,18 +196,20 @@ def test_staged_prehash_default_pool(parts, backend):
 
 def test_staged_ramp_hides_the_prehash_behind_uploads():
     """StagedOptions::first_wave_parts on the box: 128 parts at -n 5, waves
-    4, 8, 16, 32, 64, 4 pipelined against 5 ms uploads.  The first wave,
-    which the first upload waits for, is routed for speed (the CPU); the
-    rest are pre-hashed behind uploads and go out as background batches
-    (QSMD5_FLAG_BACKGROUND: the GPU, leaving the host's cores free).  Every
-    digest is golden, and the uploader waits for little more than the first
-    wave."""
+    4, 8, 16, 32, 64, 4 pipelined against 10 ms uploads.  The first wave,
+    which the first upload waits for, is routed for speed (the CPU), and so
+    is every wave whose GPU time (~85 ms chain plus reads) the uploads of
+    the wave before it cannot cover (round 6: the 8- and 16-part waves
+    behind 40 and 80 ms of uploads); the rest are pre-hashed behind uploads
+    and go out as background batches (QSMD5_FLAG_BACKGROUND: the GPU,
+    leaving the host's cores free).  Every digest is golden, and the
+    uploader waits for little more than the first wave."""
     gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
     r = run(["--aligned", "--size=%d" % (128 * 10 * MiB), "--pool=5", "--pinned", "--staged",
-             "--wave-parts=64", "--first-wave=4", "--upload-ms=5"], "auto", timeout=600)
+             "--wave-parts=64", "--first-wave=4", "--upload-ms=10"], "auto", timeout=600)
     assert r["md5"] == gold[:128] and r["pool_free_after"] == 5 and r["uploaded"] == 128
     assert r["waves"] == 6 and r["widest_wave"] == 64, r
-    assert r["cpu_waves"] == 1 and r["gpu_waves"] == 5, r
+    assert r["gpu_waves"] >= 3 and r["cpu_waves"] >= 1, r
     assert r["wait_s"] < 0.5 * r["hash_s"], (r["wait_s"], r["hash_s"])
     print("ramp: %d waves (gpu %d, cpu %d), hash %.3f s, uploader waited %.3f s, wall %.3f s"
           % (r["waves"], r["gpu_waves"], r["cpu_waves"], r["hash_s"], r["wait_s"], r["wall_s_runs"][-1]))
