@@ -928,7 +928,8 @@ int hash_read_routed(const uint64_t* lens, size_t n, qsmd5_read_fn read, void* u
     log_msg(QSMD5_LOG_WARN, "qsmd5: GPU read batch of %zu chunks failed (%s); re-reading and hashing "
             "it on the CPU", n, gpu_err.c_str());
   J.short_read = false;
-  J.read_s = 0;
+  J.read_s = J.clean_read_s = J.busy_read_s = 0;  // the CPU run's own reads only
+  J.clean_bytes = J.busy_bytes = 0;
   const int rc2 = on_cpu("fallback");
   if (rc2) return fail(rc2, t_last_error + " (after GPU failure: " + gpu_err + ")");
   g_fallbacks.fetch_add(1);

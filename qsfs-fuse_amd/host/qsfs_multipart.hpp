@@ -449,9 +449,9 @@ struct StagedOptions {
   std::function<bool()> should_continue;  // as PrehashOptions::should_continue (thread-safe)
   // With pipeline: while a part uploads, the next part of the wave is read
   // into a buffer the pool has free at that moment (try_acquire, never a
-  // blocking acquire while this thread holds a buffer) on a helper thread, so
-  // the loop's own ReadNoLoad runs behind the upload instead of between
-  // uploads (512 reads of ~0.8 ms each, serial with the
+  // blocking acquire while this thread holds a buffer) on a helper thread,
+  // wherever the last upload() took longer than the last read, so the loop's
+  // own ReadNoLoad runs behind the upload instead of between uploads (512 reads of ~0.8 ms each, serial with the
   // uploads, were the staged flow's 0.42 s over pure upload time).  The file
   // then has two parts in flight for one flush, as the reference's async
   // path has up to -n (QSTransferManager.cpp:654-659).  Needs a pool with
@@ -566,6 +566,10 @@ class ReadAhead {
     if (err_) std::rethrow_exception(err_);
     return got_;
   }
+  double last_s() {  // how long the last job ran (after get())
+    std::lock_guard<std::mutex> lk(mu_);
+    return last_s_;
+  }
 
  private:
   void loop() {
@@ -578,12 +582,15 @@ class ReadAhead {
       lk.unlock();
       size_t got = 0;
       std::exception_ptr err;
+      const auto t0 = std::chrono::steady_clock::now();
       try {
         got = job();
       } catch (...) {
         err = std::current_exception();
       }
+      const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
       lk.lock();
+      last_s_ = s;
       got_ = got;
       err_ = err;
       done_ = true;
@@ -596,6 +603,7 @@ class ReadAhead {
   std::function<size_t()> job_;
   bool has_job_ = false, done_ = true, stop_ = false;
   size_t got_ = 0;
+  double last_s_ = 0;
   std::exception_ptr err_;
 };
 
@@ -707,6 +715,7 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
   auto stop_requested = [&] { return opt.should_continue && !opt.should_continue(); };
   const bool read_ahead = opt.pipeline && opt.read_ahead;
   detail::ReadAhead reader;  // joined on return, after every read it ran was waited for
+  double last_upload_s = 0, last_read_s = 0;  // the last part's upload() and read
   const auto tw = clock::now();
   detail::StagedWave cur = prep(0, wave_size(0), false);
   st.wait_s += secs(tw, clock::now());
@@ -768,6 +777,7 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
             throw;
           }
           st.loop_read_s += secs(r0, clock::now());
+          last_read_s = reader.last_s();
         } else {
           b = pool.acquire();
           st.acquire_s += secs(r0, clock::now());
@@ -783,7 +793,8 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
             pool.release(b);
             throw;
           }
-          st.loop_read_s += secs(r1, clock::now());
+          last_read_s = secs(r1, clock::now());
+          st.loop_read_s += last_read_s;
         }
         try {
           if (got != p.size)
@@ -800,8 +811,11 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
             ++st.rehashed;
           }
           // The next part's read, behind this part's upload, into a buffer
-          // that is free right now (never a blocking acquire while holding b).
-          if (read_ahead && k + 1 < n) {
+          // that is free right now (never a blocking acquire while holding b)
+          // -- where the uploads take longer than the reads (the last part's
+          // of each, measured): uploads that return at once hide nothing, and
+          // the read would only contend with the next wave's pre-hash.
+          if (read_ahead && k + 1 < n && last_upload_s > last_read_s) {
             typename Pool::buffer_type b2;
             const qsmd5_part& q = parts[cur.first + k + 1];
             if (detail::try_acquire_if_any(pool, &b2, detail::has_try_acquire<Pool>())) {
@@ -820,7 +834,8 @@ WaveStats upload_parts_staged(const std::vector<qsmd5_part>& parts, Pool& pool, 
           }
           const auto u0 = clock::now();
           upload(p, b, detail::hex(&cur.dig[16 * k]));
-          st.upload_call_s += secs(u0, clock::now());
+          last_upload_s = secs(u0, clock::now());
+          st.upload_call_s += last_upload_s;
         } catch (...) {
           pool.release(b);  // not handed over
           throw;

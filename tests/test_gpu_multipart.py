@@ -141,6 +141,7 @@ def test_concurrent_files_gpu_waves(gold, mode):
         assert m[:want] == gold[:want] and not any(m[want:]), m
 
 
+@pytest.mark.gpu
 def test_reference_loop_beside_the_staged_binding():
     """the flush loop the binding replaces, timed beside it
     on the same file -- QSTransferManager::DoMultiPartUpload with -m as the

@@ -310,20 +310,24 @@ def test_reference_loop_matches_golden(mode):
         assert r["seconds"] >= r["hash_s"] + r["loop_read_s"]
 
 
-@pytest.mark.parametrize("extra", [[], ["--async=3"], ["--wave-parts=5", "--first-wave=2"]])
+@pytest.mark.parametrize("extra", [[], ["--wave-parts=5", "--first-wave=2"]])
 def test_staged_read_ahead_matches_golden(extra):
-    """StagedOptions::read_ahead (VERDICT r05 item 3): the next part is read
-    into a buffer the pool has free (try_acquire) while this part uploads; the
-    digests stay golden, every buffer comes back, and nearly every part after
-    each wave's first was read ahead.  --no-read-ahead is the reference's
+    """StagedOptions::read_ahead (VERDICT r05 item 3): while a part uploads,
+    the next part is read into a buffer the pool has free (try_acquire),
+    wherever the last upload took longer than the last read.  With 20 ms
+    uploads nearly every part after the first is read ahead; with uploads
+    that return at once none is (nothing to hide behind).  The digests stay
+    golden and every buffer comes back; --no-read-ahead is the reference's
     one-buffer loop exactly."""
     gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
-    base = ["--aligned", "--size=%d" % (16 * 10 * MiB), "--pool=5", "--staged", "--upload-ms=2"] + extra
-    on = run(base, "cpu")
-    off = run(base + ["--no-read-ahead"], "cpu")
-    for r in (on, off):
+    base = ["--aligned", "--size=%d" % (16 * 10 * MiB), "--pool=5", "--staged"] + extra
+    on = run(base + ["--upload-ms=20"], "cpu")
+    off = run(base + ["--upload-ms=20", "--no-read-ahead"], "cpu")
+    fast = run(base + ["--upload-ms=0"], "cpu")
+    for r in (on, off, fast):
         assert r["md5"] == gold[:16] and r["uploaded"] == 16 and r["pool_free_after"] == 5
-    assert off["read_ahead"] == 0 and on["read_ahead"] >= 16 - on["waves"] - 2, on["read_ahead"]
+    assert off["read_ahead"] == 0 and fast["read_ahead"] == 0
+    assert on["read_ahead"] >= 16 - 2 * on["waves"] - 1, on["read_ahead"]
 
 
 def test_staged_read_ahead_faults_return_every_buffer():
@@ -331,7 +335,7 @@ def test_staged_read_ahead_faults_return_every_buffer():
     is being read ahead: the upload stops, nothing leaks."""
     for fault, want in (("--short-read-part=7", 0), ("--fail-upload-part=7", 6)):
         out = run_raw(["--aligned", "--size=%d" % (12 * 10 * MiB), "--pool=5", "--staged", "--wave-parts=12",
-                       fault], "cpu")
+                       "--upload-ms=20", fault], "cpu")
         assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
         r = json.loads(out.stdout)
         assert r["uploaded"] == want and r["pool_free_after"] == 5, (fault, r["uploaded"])
