@@ -75,12 +75,14 @@ def test_binding_as_printed(doctest_exe, cancel_after, flush):
 
 @pytest.mark.parametrize("flush", ["async", "sync"])
 def test_write_during_the_upload_rehashes_the_part(doctest_exe, flush):
-    """Another descriptor writes the next part to go out after 3 parts went
-    out: the stored digest of that part no longer matches its bytes, so the
+    """Another descriptor writes the part after the next to go out once 2
+    parts went out (part 4 of the first wave of 4, pre-hashed before the
+    uploads began; the next one may already be read ahead): the stored
+    digest of that part no longer matches its bytes, so the
     binding (source_changed over File's write counter) re-hashes it from its
     buffer; every Content-MD5 the SDK gets is the MD5 of the bytes it gets."""
     env = dict(os.environ, QSMD5_BACKEND="cpu")
-    out = subprocess.run([doctest_exe, str(132 * MiB), str(2 * MiB), "5", "-1", flush, "3"],
+    out = subprocess.run([doctest_exe, str(132 * MiB), str(2 * MiB), "5", "-1", flush, "2"],
                          env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stdout + out.stderr[-3000:]
     r = json.loads(out.stdout.strip().splitlines()[-1])
@@ -105,7 +107,7 @@ def test_write_during_the_upload_negative_control(tmp_path):
         "-L" + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-lqsmd5", "-lpthread",
         "-Wl,-rpath," + os.path.join(ROOT, "qsfs-fuse_amd", "lib"), "-o", exe])
     env = dict(os.environ, QSMD5_BACKEND="cpu")
-    out = subprocess.run([exe, str(132 * MiB), str(2 * MiB), "5", "-1", "async", "3"],
+    out = subprocess.run([exe, str(132 * MiB), str(2 * MiB), "5", "-1", "async", "2"],
                          env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 1 and "MD5 of the bytes sent" in out.stderr, (out.returncode, out.stderr[-2000:])
 
