@@ -413,9 +413,11 @@ WaveStats upload_parts_prehashed(const std::vector<qsmd5_part>& parts, Pool& poo
 // bytes from the caller's File::ReadNoLoad (File.cpp:308-375) in column
 // windows through the library's own bounded pinned staging, so one call hashes
 // every queued part of the file as one GPU batch.  Each digest then rides on
-// its part into the reference's loop, unchanged: one pool buffer at a time
-// (Acquire blocks while this thread holds none), ReadNoLoad into it,
-// UploadMultipart with the stored digest (QSTransferManager.cpp:602-673).
+// its part into the reference's loop: one pool buffer per part (Acquire
+// blocks only while this thread holds none), ReadNoLoad into it,
+// UploadMultipart with the stored digest (QSTransferManager.cpp:602-673) --
+// plus, round 6, the next part read into a second buffer behind the upload
+// when one is free at that instant (StagedOptions::read_ahead).
 
 struct StagedOptions {
   uint64_t staging_bytes = 0;  // qsmd5_hash_read's budget (0: QSMD5_READ_STAGING_BYTES, 256 MiB)

@@ -298,12 +298,16 @@ def _harness_golden(r, parts):
 def test_auto_prehash_matches_forced_gpu(parts):
     """the whole-file pre-hash (qsfs's -n 5 pool, the
     staged binding) under the default auto routing must run as fast as forced
-    GPU whenever auto picks the GPU: within 5% on the best of four passes,
-    every digest golden.  Round 5's gap was the read slot's buffers (65-80 ms
-    of pinned and device allocation) landing in the first GPU job, which
-    under auto often follows CPU-routed ones; they are now made at init.
-    Forced CPU runs too, and auto's best pass is within 15% of the faster
-    backend's.  QSMD5_TRACE=1 shows where each call's time went."""
+    GPU whenever auto picks the GPU.  Round 5's gap was the read slot's
+    buffers (65-80 ms of pinned and device allocation) landing in the first
+    GPU job, which under auto often follows CPU-routed ones; they are now made
+    at init.  A GPU job here is bound by the caller's reads (the page-cache
+    memcpy, which varies by ~10% from process to process on the box), so
+    what auto can add is its own part: each call's time outside the caller's
+    reads (routing, slot, setup, waits, tail).  Auto's best GPU call must
+    spend at most 5% (+ 2 ms) more there than forced GPU's best.  Forced CPU
+    runs too, and auto's best pass is within 15% of the faster backend's.
+    Every digest golden; QSMD5_TRACE=1 shows where each call's time went."""
     args = ["--aligned", "--size=%d" % (parts * 10 * MiB), "--pool=5", "--pinned", "--staged", "--repeat=4"]
     best, picks = {}, {}
     for backend in ("gpu", "cpu", "auto"):
@@ -314,11 +318,13 @@ def test_auto_prehash_matches_forced_gpu(parts):
         assert len(traces) == 4
         picks[backend] = traces
         best[backend] = min(t["total_ms"] for t in traces)
-        print("%s %d parts: pre-hash calls %s" % (backend, parts, [
+        print("%s %d parts: pre-hash calls (backend, reason, total ms, reads ms) %s" % (backend, parts, [
             (t["backend"], t["reason"], round(t["total_ms"], 1), round(t["read_ms"], 1)) for t in traces]))
-    auto_gpu = [t["total_ms"] for t in picks["auto"] if t["backend"] == "gpu"]
+    own = lambda ts: min(t["total_ms"] - t["read_ms"] for t in ts)  # noqa: E731
+    auto_gpu = [t for t in picks["auto"] if t["backend"] == "gpu"]
     if auto_gpu:
-        assert min(auto_gpu) <= 1.05 * best["gpu"], (min(auto_gpu), best["gpu"])
+        print("outside the reads: auto %.1f ms, forced GPU %.1f ms" % (own(auto_gpu), own(picks["gpu"])))
+        assert own(auto_gpu) <= 1.05 * own(picks["gpu"]) + 2.0, (own(auto_gpu), own(picks["gpu"]))
     assert best["auto"] <= 1.15 * min(best["gpu"], best["cpu"]), best
 
 
