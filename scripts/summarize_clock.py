@@ -2,7 +2,8 @@
 pass (counter_collection CSV): GRBM_GUI_ACTIVE is summed over the 8 XCDs, so
 busy cycles = value / 8, and clock = busy cycles / the dispatch's wall time
 (MI355X_MICROARCH.md, 'DVFS give-back'; within ~3% of the in-kernel clock on
-dispatches of 10 ms or more).
+dispatches of 10 ms or more; dispatches under 1 ms are skipped: the counter's
+granularity makes their figure meaningless).
 
 usage: python3 summarize_clock.py <counter_collection.csv> [title]
 """
@@ -24,7 +25,7 @@ def main():
     print(title)
     for d in sorted(rows):
         name, active, wall = rows[d]
-        if wall <= 0:
+        if wall < 1e-3:
             continue
         print("  dispatch %3d %-32s %8.3f ms  GRBM_GUI_ACTIVE %.4g  -> %.3f GHz"
               % (d, name[:32], wall * 1e3, active, active / 8.0 / wall / 1e9))
