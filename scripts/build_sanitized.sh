@@ -7,6 +7,7 @@
 # are the product's own object.
 #   qsfs-fuse_amd/lib/san/race_stress_tsan   runtime + test under ThreadSanitizer
 #   qsfs-fuse_amd/lib/san/race_stress_asan   runtime + test under AddressSanitizer + UBSan
+#   qsfs-fuse_amd/lib/san/nested_read_{tsan,asan}  tests/cpp/nested_read.cpp over the same runtime
 # Builds in this container (hipcc cross-compiles); runs on the GPU box
 # (tests/test_gpu_sanitizers.py).
 set -euo pipefail
@@ -37,5 +38,10 @@ for v in tsan asan; do
   $CXX $SAN -o "$OUT/race_stress_$v" "$OUT/race_stress_$v.o" $RT_OBJS "$OUT/md5_cpu_$v.o" "$OUT/md5_cpu_mb_$v.o" \
     "$R/qsfs-fuse_amd/lib/md5_kernels.o" "$OUT/md5_oracle_$v.o" \
     -L/opt/rocm/lib -lamdhip64 -lpthread -Wl,-rpath,/opt/rocm/lib
+  # read callbacks calling back into the library (round 6):
+  # reader crews, nested calls, a shutdown pending meanwhile
+  $CXX -O1 -g -std=c++17 $SAN -c "$R/tests/cpp/nested_read.cpp" -o "$OUT/nested_read_$v.o"
+  $CXX $SAN -o "$OUT/nested_read_$v" "$OUT/nested_read_$v.o" $RT_OBJS "$OUT/md5_cpu_$v.o" "$OUT/md5_cpu_mb_$v.o" \
+    "$R/qsfs-fuse_amd/lib/md5_kernels.o" -L/opt/rocm/lib -lamdhip64 -lpthread -Wl,-rpath,/opt/rocm/lib
 done
-echo "sanitized builds: $OUT/race_stress_tsan $OUT/race_stress_asan"
+echo "sanitized builds: $OUT/race_stress_tsan $OUT/race_stress_asan $OUT/nested_read_tsan $OUT/nested_read_asan"

@@ -218,3 +218,32 @@ def test_tsan_negative_control_reports_planted_race():
     assert "WARNING: ThreadSanitizer: data race" in text, text[-3000:]
     assert "race_stress.cpp" in text and "worker" in text, text[-3000:]
     assert rc == 66, rc  # TSAN_OPTIONS exitcode: the report fails the run
+
+
+@pytest.mark.gpu
+@pytest.mark.cpu_backend
+@pytest.mark.parametrize("variant", ["tsan", "asan"])
+@pytest.mark.parametrize("args,slots", [(["shutdown", "gpu"], "4"), (["nested-read", "gpu", "auto"], "1"),
+                                        (["nested-read", "gpu", "gpu"], "1")],
+                         ids=["parallel_readers_shutdown", "nested_auto", "nested_gpu_edeadlk"])
+def test_nested_read_callbacks_under_sanitizers(variant, args, slots):
+    """tests/cpp/nested_read.cpp over the instrumented runtime (round 6,
+    ADVICE r05): the outer pull-driven batch on the GPU, its read callbacks on
+    the calling thread and the reader crew calling back into the library --
+    qsmd5_hash_one while a shutdown is pending, or a nested qsmd5_hash_read
+    (CPU under auto; -EDEADLK when forced onto the GPU's only, busy slot).
+    No deadlock, every digest right, no sanitizer report."""
+    exe = os.path.join(SAN, "nested_read_" + variant)
+    if not os.path.exists(exe):
+        pytest.fail("%s missing: run scripts/build_sanitized.sh" % exe)
+    env = dict(os.environ, QSMD5_BACKEND="auto", QSMD5_READ_SLOTS=slots,
+               ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=23",
+               TSAN_OPTIONS="halt_on_error=0:exitcode=66:second_deadlock_stack=1:suppressions=" +
+               os.path.join(ROOT, "tests", "cpp", "tsan_hip.supp"))
+    out = _watch([exe] + args, env)
+    text = out.stdout + out.stderr
+    for m in REPORT_MARKERS:
+        at = text.find(m)
+        assert at < 0, text[max(0, at - 200):at + 8000]
+    assert out.returncode == 0 and '"deadlock": false' in out.stdout, text[-4000:]
+

@@ -61,3 +61,23 @@ def test_tsan_negative_control_cpu_backend():
                          capture_output=True, text=True, timeout=300)
     assert "WARNING: ThreadSanitizer: data race" in out.stderr, (out.stdout + out.stderr)[-3000:]
     assert out.returncode == 66
+
+
+@pytest.mark.parametrize("variant", ["tsan", "asan"])
+@pytest.mark.parametrize("args", [["shutdown", "cpu"], ["shutdown", "auto"], ["nested-read", "cpu", "auto"]],
+                         ids=["parallel_readers_shutdown_cpu", "parallel_readers_shutdown_auto", "nested_read"])
+def test_nested_read_callbacks_cpu_backend(variant, args):
+    """tests/cpp/nested_read.cpp (round 6) over the runtime built
+    with ThreadSanitizer, and with AddressSanitizer + UBSan, on the library's
+    CPU path: the window's rows read by the reader crew, whose callbacks call
+    qsmd5_hash_one while a shutdown is pending, or nested qsmd5_hash_read
+    calls.  No deadlock, every digest right, no sanitizer report."""
+    exe = os.path.join(SAN, "nested_read_" + variant)
+    assert os.path.exists(exe), "run __graft_entry__.build() (scripts/build_sanitized.sh)"
+    env = dict(os.environ, QSMD5_BACKEND="auto", ASAN_OPTIONS="detect_leaks=0", TSAN_OPTIONS=TSAN)
+    out = subprocess.run(["setarch", "x86_64", "-R", exe] + args, env=env, capture_output=True, text=True,
+                         timeout=300)
+    text = out.stdout + out.stderr
+    assert "Sanitizer" not in text and "runtime error" not in text, text[-4000:]
+    assert out.returncode == 0 and '"deadlock": false' in out.stdout, text[-3000:]
+
