@@ -279,12 +279,19 @@ struct SlotLease {
   }
 };
 
-// Staging regions per job on the GPU path (QSMD5_READ_REGIONS, 2..4, default
-// 2): the budget is split into that many host regions (and as many device
-// regions with the overlap), so a window is budget / regions wide and up to
-// regions - 1 windows are in flight behind the one being read.
-int read_regions() {
-  return (int)std::min<uint64_t>(kMaxReadRegions, std::max<uint64_t>(2, env_u64("QSMD5_READ_REGIONS", 2)));
+// Staging regions per job on the GPU path (QSMD5_READ_REGIONS, 2..4): the
+// budget is split into that many host regions (and as many device regions
+// with the overlap), so a window is budget / regions wide and up to
+// regions - 1 windows are in flight behind the one being read.  By default 2
+// for a job read on one thread and 4 for one read by parallel readers: on the
+// MI355X box (profiles/r06_flush_sweep_tree.jsonl, 512 x 10 MiB) 4 readers
+// ran at 48 GiB/s with 4 regions, steadily, against 46 at best and 34-42
+// often with 2, while one reader ran at 21 GiB/s with 2 regions and 13-17
+// with 4 (narrower windows of page-cache gathers).  Either way the budget's
+// bytes are the same, so read slot 0's pre-allocation fits both.
+int read_regions(size_t readers) {
+  const uint64_t dflt = readers > 1 ? 4 : 2;
+  return (int)std::min<uint64_t>(kMaxReadRegions, std::max<uint64_t>(2, env_u64("QSMD5_READ_REGIONS", dflt)));
 }
 
 // Metadata bytes of a job of n chunks over `dregions` device regions: one
@@ -334,7 +341,7 @@ int gpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
   if (int rc = lease.ready(&slot)) return rc;
   ReadSlot& rs = *slot;
   const bool overlap = env_u64("QSMD5_READ_OVERLAP", 1) != 0;
-  const int R = read_regions();
+  const int R = read_regions(J.readers);
   const int dregions = overlap ? R : 1;
   const size_t n = J.len.size();
   const ReadPlan P = plan_read(J.sorted, 2 * staging / R);  // regions of staging / R
@@ -736,7 +743,7 @@ void note_read_rate(const ReadJob& J) {
 // the last window's copy and column kernel after its read.  Chains of one
 // group run as long as its longest chunk; groups run one after another.
 double gpu_read_est_ms(const ReadJob& J, uint64_t staging, double read_ms) {
-  const ReadPlan P = plan_read(J.sorted, 2 * staging / read_regions());
+  const ReadPlan P = plan_read(J.sorted, 2 * staging / read_regions(J.readers));
   const double chain = gpu_chain_gibs();
   double chain_ms = 0, tail_ms = 0;
   for (const ReadGroup& g : P.groups) {
@@ -779,7 +786,7 @@ void prewarm_read_slot(Dev& d) {
   for (hipEvent_t* ev : rs.events())
     if (!*ev && (e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) *ev = nullptr;
   const uint64_t staging = env_u64("QSMD5_READ_STAGING_BYTES", kDefaultReadStaging);
-  const int R = read_regions();
+  const int R = read_regions(1);
   const uint64_t region = std::max<uint64_t>(staging / R, stage_bytes(kReadColMin));  // gpu_read's plan
   const int dregions = env_u64("QSMD5_READ_OVERLAP", 1) ? R : 1;
   constexpr size_t n = 4096;
