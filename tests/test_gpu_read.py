@@ -301,30 +301,31 @@ def test_auto_prehash_matches_forced_gpu(parts):
     GPU whenever auto picks the GPU.  Round 5's gap was the read slot's
     buffers (65-80 ms of pinned and device allocation) landing in the first
     GPU job, which under auto often follows CPU-routed ones; they are now made
-    at init.  A GPU job here is bound by the caller's reads (the page-cache
-    memcpy, which varies by ~10% from process to process on the box), so
-    what auto can add is its own part: each call's time outside the caller's
-    reads (routing, slot, setup, waits, tail).  Auto's best GPU call must
-    spend at most 5% (+ 2 ms) more there than forced GPU's best.  Forced CPU
-    runs too, and auto's best pass is within 15% of the faster backend's.
-    Every digest golden; QSMD5_TRACE=1 shows where each call's time went."""
-    args = ["--aligned", "--size=%d" % (parts * 10 * MiB), "--pool=5", "--pinned", "--staged", "--repeat=4"]
-    best, picks = {}, {}
-    for backend in ("gpu", "cpu", "auto"):
-        r = run(args, backend, timeout=600, extra_env={"QSMD5_TRACE": "1"})
-        _harness_golden(r, parts)
-        traces = [json.loads(l.split("qsmd5 read trace: ", 1)[1]) for l in r["_stderr"].splitlines()
-                  if "qsmd5 read trace: " in l]
-        assert len(traces) == 4
-        picks[backend] = traces
-        best[backend] = min(t["total_ms"] for t in traces)
-        print("%s %d parts: pre-hash calls (backend, reason, total ms, reads ms) %s" % (backend, parts, [
-            (t["backend"], t["reason"], round(t["total_ms"], 1), round(t["read_ms"], 1)) for t in traces]))
-    own = lambda ts: min(t["total_ms"] - t["read_ms"] for t in ts)  # noqa: E731
-    auto_gpu = [t for t in picks["auto"] if t["backend"] == "gpu"]
+    at init.  The passes interleave in ONE process (--backends: cpu, gpu, cpu,
+    auto, ...), so every backend sees the same pages, the same NUMA placement
+    and the same GPU clock history -- across processes the page-cache reads
+    alone vary by 10-30% on the two-socket box.  Auto's best GPU pass must be
+    within 5% of forced GPU's best, and auto's best pass within 15% of the
+    faster backend's.  Every pass hands on the same digests, the last golden;
+    QSMD5_TRACE=1 shows where each call's time went."""
+    order = ["cpu", "gpu", "cpu", "auto"]
+    r = run(["--aligned", "--size=%d" % (parts * 10 * MiB), "--pool=5", "--pinned", "--staged", "--repeat=16",
+             "--backends=" + ",".join(order)], "auto", timeout=600, extra_env={"QSMD5_TRACE": "1"})
+    _harness_golden(r, parts)
+    assert r["pass_mismatch"] == 0
+    traces = [json.loads(l.split("qsmd5 read trace: ", 1)[1]) for l in r["_stderr"].splitlines()
+              if "qsmd5 read trace: " in l]
+    assert len(traces) == 16
+    by = {"gpu": [], "cpu": [], "auto": []}
+    for k, t in enumerate(traces):
+        by[order[k % len(order)]].append(t)
+    for b in ("gpu", "cpu", "auto"):
+        print("%s %d parts: pre-hash calls (backend, reason, total ms, reads ms) %s" % (b, parts, [
+            (t["backend"], t["reason"], round(t["total_ms"], 1), round(t["read_ms"], 1)) for t in by[b]]))
+    best = {b: min(t["total_ms"] for t in by[b]) for b in by}
+    auto_gpu = [t["total_ms"] for t in by["auto"] if t["backend"] == "gpu"]
     if auto_gpu:
-        print("outside the reads: auto %.1f ms, forced GPU %.1f ms" % (own(auto_gpu), own(picks["gpu"])))
-        assert own(auto_gpu) <= 1.05 * own(picks["gpu"]) + 2.0, (own(auto_gpu), own(picks["gpu"]))
+        assert min(auto_gpu) <= 1.05 * best["gpu"], (min(auto_gpu), best["gpu"])
     assert best["auto"] <= 1.15 * min(best["gpu"], best["cpu"]), best
 
 

@@ -369,3 +369,16 @@ def test_read_callbacks_call_back_into_the_library(tmp_path, args):
         assert r["reader_thread_reads"] > 0 and r["shutdown_rc"] == 0
     else:
         assert r["nested_ok"] == r["nested_calls"] > 0
+
+
+def test_backends_alternate_per_pass_in_one_process():
+    """--backends=cpu,auto: the harness sets QSMD5_BACKEND before each pass
+    (the library reads it at each call), so backends can be compared in one
+    process; every pass hands on the same golden digests."""
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    r = run(["--aligned", "--size=%d" % (8 * 10 * MiB), "--pool=5", "--staged", "--repeat=4",
+             "--backends=cpu,auto"], "cpu", extra_env={"QSMD5_TRACE": "1"})
+    assert r["md5"] == gold[:8] and r["pass_mismatch"] == 0
+    reasons = [json.loads(l.split("qsmd5 read trace: ", 1)[1])["reason"] for l in r["_stderr"].splitlines()
+               if "qsmd5 read trace: " in l]
+    assert len(reasons) == 4 and reasons[0] == reasons[2] == "forced" and reasons[1] != "forced", reasons
