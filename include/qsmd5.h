@@ -323,7 +323,9 @@ QSMD5_API int qsmd5_hash_parts(const void* file, const qsmd5_part* parts, size_t
  * split into QSMD5_READ_REGIONS regions (default 2); slot 0 of the primary
  * GPU is taken at initialisation unless QSMD5_READ_PREWARM=0, the others on
  * first use, all kept until qsmd5_shutdown); a further call waits for a
- * slot.  One bound GPU
+ * slot.  The CPU path's pageable staging (up to staging_bytes per call) is
+ * likewise kept for the next call, up to QSMD5_READ_SLOTS buffers, until
+ * qsmd5_shutdown.  One bound GPU
  * hashes a whole call: the one with the fewest such calls in flight (the
  * first on a tie), so with QSMD5_DEVICES binding several, files flushed at
  * once spread over the GPUs. */
