@@ -505,10 +505,13 @@ struct CpuStagingCache {
   std::mutex mu;
   std::vector<std::pair<size_t, uint8_t*>> free;  // (bytes, buffer)
 };
-CpuStagingCache& cpu_staging_cache() {
-  static CpuStagingCache* c = new CpuStagingCache;  // leaked, as rt()
-  return *c;
-}
+// Constructed when the library loads, not at first use: a function-local
+// static's lazy initialisation is published by an inline guard check that a
+// ThreadSanitizer build of a caller cannot see inside this (uninstrumented)
+// library, which then reports the first two callers' use of the mutex as a
+// race (tests/test_multipart_cpu.py, staged flow under TSan).
+CpuStagingCache g_cpu_staging_cache;
+CpuStagingCache& cpu_staging_cache() { return g_cpu_staging_cache; }
 
 class CpuStaging {
  public:

@@ -382,3 +382,29 @@ def test_backends_alternate_per_pass_in_one_process():
     reasons = [json.loads(l.split("qsmd5 read trace: ", 1)[1])["reason"] for l in r["_stderr"].splitlines()
                if "qsmd5 read trace: " in l]
     assert len(reasons) == 4 and reasons[0] == reasons[2] == "forced" and reasons[1] != "forced", reasons
+
+
+@pytest.mark.parametrize("mode", [[], ["--wave-parts=4", "--first-wave=2"], ["--async=3"], ["--cancel-after=5"]],
+                         ids=["whole", "ramp", "async", "cancel"])
+def test_staged_concurrent_files_under_tsan(mode):
+    """The staged binding's threads under ThreadSanitizer (round 6): the
+    pre-hash helper, the upload loop's read-ahead thread, the shared pool and
+    the executor's handler, four files at once through one 5-buffer pool with
+    uploads slow enough (30 ms) that the read-ahead runs (not with the
+    executor, whose upload() returns at once).  No report, every digest
+    golden, every buffer back."""
+    exe = build_tsan()
+    gold = json.load(open(os.path.join(GOLDEN, "batch_10MiB.json")))["md5"]
+    env = dict(os.environ, QSMD5_BACKEND="cpu", TSAN_OPTIONS="halt_on_error=0:exitcode=66:suppressions="
+               + os.path.join(ROOT, "tests", "cpp", "tsan_hip.supp"))
+    out = subprocess.run(["setarch", "x86_64", "-R", exe, "--aligned", "--size=%d" % (8 * 10 * MiB),
+                          "--pool=5", "--files=4", "--upload-ms=30", "--deadlock-s=30", "--staged"] + mode,
+                         env=env, capture_output=True, text=True, timeout=300)
+    assert "WARNING: ThreadSanitizer" not in out.stderr, out.stderr[-8000:]
+    assert out.returncode == 0, out.stderr[-3000:]
+    r = json.loads(out.stdout)
+    want = 5 if "--cancel-after=5" in mode else 8
+    assert r["deadlock"] is False and r["pool_free_after"] == 5, r
+    assert all(m[:want] == gold[:want] and not any(m[want:]) for m in r["md5_files"]), r["md5_files"]
+    if "--cancel-after=5" not in mode and "--async=3" not in mode:  # an executor's upload() returns at once
+        assert r["read_ahead"] > 0, r["read_ahead"]
