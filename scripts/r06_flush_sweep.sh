@@ -53,6 +53,15 @@ for P in ${PARTS:-128 512}; do
       run "staged_whole_u${U}_P$P" --size=$S --pool=5 --pinned --staged --upload-ms=$U --repeat=2 || exit 1
     done
   fi
+  if [[ $CASES == all || $CASES == *sync* ]]; then
+    # qsfs's default mode (qsSingleThread, Parser.cpp:286): File::Flush uploads
+    # synchronously under the file's lock (File.cpp:619, 641-643), so the
+    # binding runs without its helper thread (pipeline off: the whole file
+    # pre-hashed on the flushing thread, no read-ahead)
+    for U in 0 10; do
+      run "staged_sync_u${U}_P$P" --size=$S --pool=5 --pinned --staged --no-pipeline --upload-ms=$U --repeat=2 || exit 1
+    done
+  fi
   if [[ $CASES == all || $CASES == *files* ]] && [[ $P == 128 ]]; then
     # four files flushed at once from four threads through one 5-buffer pool
     run "staged_4files_ramp_u0_P$P" --size=$S --pool=5 --pinned --staged --files=4 --wave-parts=32 --repeat=2 || exit 1

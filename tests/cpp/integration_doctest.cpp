@@ -14,10 +14,11 @@
 // failed, and every buffer is back in the pool.
 //
 // usage: integration_doctest <file_bytes> <part_bytes> <pool_buffers> <cancel_after|-1> [flush] [write_after]
-//   flush: async (default: File::Flush submitted the upload and returned, no
-//   lock held), sync (the flushing thread holds the file's lock through the
-//   upload and sets the flag, as File::Flush's synchronous branch with the
-//   binding's addition), sync_unflagged (the negative control: the lock held,
+//   flush: async (this program's default; qsfs's -M mode: File::Flush
+//   submitted the upload and returned, no lock held), sync (qsfs's default
+//   single-threaded mode: the flushing thread holds the file's lock through
+//   the upload and sets the flag, as File::Flush's synchronous branch with
+//   the binding's addition), sync_unflagged (the negative control: the lock held,
 //   the flag not set -- a helper thread's read waits forever; the watchdog
 //   exits 3).  write_after: once that many parts went out, the file is
 //   written (the part after the next to go out changes) as by another descriptor.
