@@ -310,8 +310,10 @@ inline int pipeline_turn(size_t S, size_t nregions, bool meta, PipelineState& st
 // library asks for them in COLUMN WINDOWS and hashes each window as it lands,
 // every chain parking its state between windows.  The staging budget B is
 // split into two host regions (the reader fills one while the other is copied
-// to the GPU) and one device region; a region holds one column of a GROUP of
-// up to `rows_max` chunks, row k at stride stage_bytes(W).  So the GPU's width
+// to the GPU; the GPU path passes 2B / R to split it into R,
+// qsmd5_rt_read.cpp read_regions) and as many device regions; a region holds
+// one column of a GROUP of up to `rows_max` chunks, row k at stride
+// stage_bytes(W).  So the GPU's width
 // (one chain per chunk in a group) depends on the budget only through the
 // column width W, never on how many whole chunks fit: 512 x 10 MiB parts go in
 // ONE group of 512 chains through 512 MiB of staging (21 columns of 508 KiB),

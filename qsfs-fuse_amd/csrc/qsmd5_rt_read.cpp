@@ -12,17 +12,17 @@
 // loaded file), and every part of the file is its own chain, parked between
 // windows: the batch is as wide as the file, the staging stays bounded.
 //
-// Schedule on the GPU (the job's read slot: its own stream and buffers, up to
+// Schedule on the GPU (the job's read slot: its own streams and buffers, up to
 // QSMD5_READ_SLOTS jobs side by side, qsmd5_rt.h ReadSlot; qsmd5_plan.h
-// plan_read): step s = (group,
-// column).  The calling thread fills host region s % 2 through the caller's
-// reads, then enqueues its H2D copy into the one device region and the column
-// kernel that hashes it.  Stream order keeps the device region safe (copy s+1
-// runs after kernel s); the host waits only before refilling a host region, for
-// the copy that last read it (two steps back), so the reads of step s+1 run
-// while step s copies and hashes.  The reads are the bound: a column kernel of
-// 512 chains x 508 KiB runs in ~4 ms, the copy in ~5 ms, while one thread
-// gathers the 254 MiB in ~20 ms (the page cache's memcpy).
+// plan_read): step s = (group, column).  The budget is split into R staging
+// regions (read_regions below).  The calling thread fills host region s % R
+// through the caller's reads and enqueues its H2D copy into device region
+// s % R on the copy stream; the column kernel that hashes it goes on the
+// kernel stream once the host has seen that copy land (gpu_read).  So the
+// reads of window s + 1 run while window s copies and window s - 1 hashes.
+// With one reader the reads are the bound: a column kernel of 512 chains x
+// 252 KiB runs in ~2 ms, its copy in ~2.5 ms, while one thread gathers the
+// 127 MiB window in ~7 ms (the page cache's memset + memcpy, as ReadNoLoad).
 #include <array>
 #include <deque>
 #include <functional>
@@ -308,23 +308,23 @@ int event_state(hipEvent_t ev, const char* what) {
 }
 
 // The GPU backend of a pull-driven batch.  Step s = (group, column) of the
-// plan: the calling thread fills host region s % 2 through the caller's
+// plan: the calling thread fills host region s % R through the caller's
 // reads, then enqueues its H2D copy on the slot's copy stream into device
-// region s % 2; the column kernel that hashes it goes on the slot's kernel
+// region s % R; the column kernel that hashes it goes on the slot's kernel
 // stream once the host has seen that copy land (the kernels of a group run in
 // column order on that one stream: each resumes the chains the last one
 // parked).  The order between the two streams is kept by this thread, not by
 // hipStreamWaitEvent (which keeps a HIP thread polling for the whole batch:
 // DESIGN.md §5, "Host CPU of a GPU wave"), as run_batch does:
-//   - host region s % 2 is refilled once the copy that last read it (step
-//     s - 2) has landed;
-//   - device region s % 2 is overwritten once the kernel that last read it
-//     (step s - 2) has finished;
+//   - host region s % R is refilled once the copy that last read it (step
+//     s - R) has landed;
+//   - device region s % R is overwritten once the kernel that last read it
+//     (step s - R) has finished;
 //   - kernel s is launched at the first check after copy s has landed (before
-//     and after each window's reads, or when a region is needed).
+//     and after each window's reads, and right after a host region's wait).
 // So the copy of window s and the kernel of window s - 1 run while the caller
 // reads window s + 1 (with one stream, copy s + 1 queued
-// behind kernel s, ~28 GiB/s of copy + kernel, once parallel readers outran
+// behind kernel s, ~27 GiB/s of copy + kernel, once parallel readers outran
 // it).  QSMD5_READ_OVERLAP=0 keeps the round-5 order: copy and kernel on one
 // stream into one device region.
 int gpu_read(ReadJob& J, uint64_t staging, uint8_t (*digests)[16]) {
